@@ -1,0 +1,214 @@
+"""PERT step-2 SVI throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4] [--scaling strong|weak]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+A step is one full ``svi_s.step`` of reference pert_model.py:801 on the step-2
+(enumerated) model: the fused enumerated ELBO + analytic gradient + Adam pass over
+all (bin, cell) pairs of the shard, the reductions, the RCCL all-reduce of the
+shared-gradient block (N > 1), Adam on the remaining parameters and the loss read
+back to the host (the float the reference returns each step).  Inputs are resident
+in HBM before timing starts.  Metric: enumerated ELBO+grad cell.bins/s over the
+whole job = L * N_cells * K / (max over ranks of the timed wall time).
+
+Workload (configs[3] of BASELINE.json): synthetic
+pert_simulator-style data, 10,000 S-phase cells x 5,451 500 kb bins of
+notebooks/mcfrt.csv, 3 clones, P = 13, K = 4, g1_clones CN prior (weight 1e6).
+Strong scaling by default: the 10k cells are split over the ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (n_cells, subdivide, description)
+    "c4": (10000, 1, "synthetic 10k cells x 5451 x 500kb bins (BASELINE configs[3])"),
+    "c3": (2000, 1, "synthetic 2k cells x 5451 x 500kb bins (BASELINE configs[2])"),
+    "c1": (400, 1, "synthetic 400 cells x 5451 bins"),
+    "c5": (2000, 25, "synthetic 2k cells x 136275 x 20kb bins (BASELINE configs[4])"),
+}
+P, K = 13, 4
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def bytes_per_cellbin(P: int) -> int:
+    """Algorithmic HBM bytes of the fused step-2 pass per (bin, cell): reads fp32 (4) +
+    eta code uint16 (2) + pi logits, Adam m, v read (12 P) and written (12 P)."""
+    return 4 + 2 + 24 * P
+
+
+def synth(n_total: int, subdivide: int, seed: int, device):
+    """Seeded synthetic S-phase data on the GPU following pert_simulator.py:201-249."""
+    from scdna_replication_tools_amd.simulator import clone_profiles, convert_rt_units, load_bins
+    df = load_bins(subdivide=subdivide)
+    gc = df["gc"].to_numpy(np.float64)
+    rt = df["mcf7rt"].to_numpy(np.float64)
+    L = gc.shape[0]
+    prof = clone_profiles(L, 3)
+    clone = np.arange(n_total) % 3
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    cn = torch.as_tensor(prof, device=device)[:, torch.as_tensor(clone, device=device)]
+    rho = torch.as_tensor(convert_rt_units(rt), device=device)
+    tau = torch.rand(n_total, generator=g, device=device, dtype=torch.float64)
+    phi = 1.0 / (1.0 + torch.exp(-10.0 * (tau[None, :] - rho[:, None])))
+    rep = (torch.rand(phi.shape, generator=g, device=device, dtype=torch.float64) < phi).double()
+    omega = torch.exp(0.5 * torch.as_tensor(gc, device=device))[:, None]
+    lam = 0.75
+    u = 1e6 / (1.5 * L * float(cn.mean()))
+    delta = (u * cn * (1 + rep) * omega * (1 - lam) / lam).clamp(min=1.0)
+    rate = torch._standard_gamma(delta) * (lam / (1 - lam))
+    raw = torch.poisson(rate, generator=g)
+    reads = torch.floor(raw / raw.sum(0, keepdim=True) * 1e6)
+    return dict(gc=gc, reads=reads.float(), cn=cn.to(torch.int64), tau=tau.float(), clone_prof=prof, clone=clone)
+
+
+def cpu_baseline(data, n_cells: int, steps: int):
+    """The oracle (torch-CPU restatement of the tensor algebra Pyro runs: materialised
+    (2, P, L, N) enumeration, autograd, torch.optim.Adam) on a bounded cell sample."""
+    from oracle import pert_oracle as po
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(threads)
+    reads = data["reads"][:, :n_cells].cpu().to(torch.float32)
+    L = reads.shape[0]
+    states = data["cn"][:, :n_cells].cpu()
+    etas = torch.ones(L, n_cells, P)
+    etas.scatter_(2, states.unsqueeze(-1), 1e6)
+    bm = torch.zeros(1, K + 1)
+    bm[0, K - 1] = 0.5
+    prob = po.OracleProblem("step2", reads, torch.as_tensor(data["gc"], dtype=torch.float32),
+                            torch.zeros(n_cells, dtype=torch.long), 1, P, K, etas=etas,
+                            lamb=torch.tensor([0.75]), beta_means=bm,
+                            t_init=data["tau"][:n_cells].cpu().clamp(0.05, 0.95))
+    z0 = po.init_params(prob, seed=0)
+    po.fit(prob, z0, max_iter=1, min_iter=100, cell_chunk=64)          # warm-up
+    t0 = time.perf_counter()
+    po.fit(prob, z0, max_iter=steps, min_iter=100, cell_chunk=64)
+    dt = time.perf_counter() - t0
+    return {"value": L * n_cells * steps / dt, "unit": "cell*bins/s", "cores": threads, "kind": "port",
+            "sample": "{} cells x {} bins x {} SVI steps (oracle fp32, cell-chunked autograd)".format(
+                n_cells, L, steps),
+            "seconds": dt}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+    ap.add_argument("--bins-per-tile", type=int, default=0)
+    ap.add_argument("--cpu-cells", type=int, default=128)
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+        pg = dist
+
+    from scdna_replication_tools_amd.engine import EtaCodebook, PertShard
+    from scdna_replication_tools_amd.init import init_params
+
+    n_cells, subdiv, desc = CONFIGS[args.config]
+    n_total = n_cells * (world if args.scaling == "weak" else 1)
+    data = synth(n_total, subdiv, seed=0, device=device)
+    L = data["reads"].shape[0]
+    bounds = np.linspace(0, n_total, world + 1).round().astype(int)
+    n0, n1 = int(bounds[rank]), int(bounds[rank + 1])
+    reads = data["reads"][:, n0:n1].cpu().numpy()
+    states = data["cn"][:, n0:n1].cpu().numpy()
+    eta = EtaCodebook.from_states(states, 1e6, P)                     # g1_clones prior (pert_model.py:285-296)
+    bm = np.zeros((1, K + 1))
+    bm[0, K - 1] = 0.5                                                # betas [0.5, 0] of the simulator
+    t_init = np.clip(data["tau"][n0:n1].cpu().numpy(), 0.05, 0.95)
+    ploidy = eta.argmax_states().mean(0)
+    init = init_params(2, reads, np.zeros(n1 - n0, int), 1, P, K, ploidy=ploidy, t_init=t_init,
+                       beta_means=bm, seed=0)
+    allreduce = (lambda t: pg.all_reduce(t)) if pg is not None else None
+    shard = PertShard(2, reads, data["gc"], np.zeros(n1 - n0, int), 1, P, K, init, eta=eta, lamb=0.75,
+                      beta_means=bm, device=device, is_root=(rank == 0), n_cells_total=n_total,
+                      allreduce=allreduce, bins_per_tile=args.bins_per_tile)
+    del data
+    torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        shard.step()
+    if pg is not None:
+        pg.barrier()
+    torch.cuda.synchronize()
+    shard.pass_events = []
+    t0 = time.perf_counter()
+    losses = []
+    for _ in range(args.steps):
+        losses.append(shard.step())                 # includes the per-step loss read-back
+    torch.cuda.synchronize()
+    if pg is not None:
+        pg.barrier()
+    dt = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in shard.pass_events]))
+    shard.pass_events = None
+    t = torch.tensor([dt, kern_ms], dtype=torch.float64, device=device)
+    if pg is not None:
+        pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    dt, kern_ms_max = float(t[0]), float(t[1])
+
+    if rank == 0:
+        cellbins_total = L * n_total
+        value = cellbins_total * args.steps / dt
+        bpc = bytes_per_cellbin(P)
+        local_cb = L * (n1 - n0)
+        achieved = bpc * local_cb / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(args.pmc):
+            try:
+                pm = json.load(open(args.pmc))
+                if pm.get("config") == args.config and int(pm.get("cells", -1)) == n1 - n0:
+                    traffic = pm.get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        rec = {
+            "metric": "enumerated ELBO+grad cell*bins/s (10k cells x 5.5k bins, 500kb)",
+            "value": value, "unit": "cell*bins/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+            "scaling": args.scaling, "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": desc, "config": args.config, "cells": n_total, "bins": L, "P": P,
+                       "K": K, "cn_prior": "g1_clones (weight 1e6)", "parallelism": "cell-sharded x{}".format(world)},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "enum_kernel<13, STEP>", "kernel_ms": kern_ms,
+                         "bytes_per_cellbin": bpc},
+            "loss_first": losses[0], "loss_last": losses[-1],
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            data = synth(max(args.cpu_cells, 3), subdiv, seed=0, device=device)
+            rec["cpu_baseline"] = cpu_baseline(data, args.cpu_cells, args.cpu_steps)
+        else:
+            rec["cpu_baseline"] = None
+        print(json.dumps(rec), flush=True)
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

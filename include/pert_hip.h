@@ -1,0 +1,167 @@
+/* pert_hip.h -- C ABI of the MI355X PERT hot path (libpert_hip.so, gfx950).
+ *
+ * The reference has no FFI: its replaceable unit is Pyro's
+ *   svi.step(gammas, libs, data=..., etas=..., lamb=..., t_init=...) -> float
+ * (scdna_replication_tools/pert_model.py:743 step 1, :801 step 2, :868 step 3)
+ * plus the MAP decode infer_discrete(temperature=0) (:762-769, :820-827, :886-893).
+ * One SVI step of this library is the launch sequence
+ *   pert_enum_pass(PERT_MODE_STEP)   (steps 2/3)  or  pert_obs_pass()  (step 1)
+ *   pert_finalize()                  per-cell / per-bin / global gradient reductions
+ *   [all-reduce of the shared gradient block across ranks, from the host]
+ *   pert_adam()                      Adam on the packed non-pi parameters
+ * and the decode is pert_enum_pass(PERT_MODE_DECODE).
+ *
+ * Conventions: every buffer is device memory owned by the caller (allocated via
+ * the torch caching allocator on the caller's side); nothing here allocates.  All
+ * launches go on the caller's stream.  Entry points return 0 on success, a
+ * positive PERT_E* code for an argument error and 1000 + hipError_t for a launch
+ * failure.  A NaN loss is returned as data (pert_model.py:755-758), never raised.
+ *
+ * Layouts (bin-major like the reference's (loci x cells) tensors, pert_model.py:156-166):
+ *   reads      float  [L][N]       integer-valued counts
+ *   gcf        float  [L][K1]      [gc^K .. gc^1, 1] (make_gc_features, pert_model.py:460-463)
+ *   eta_code   uint16 [L][N]       row index into eta_table          (steps 2/3)
+ *   eta_table  float  [n_codes][P+1]  (eta_k - 1 for k < P, then S1 = sum_k (eta_k - 1))
+ *   z_pi/m_pi/v_pi float [L][P][N]  softmax logits of expose_pi + Adam moments, one
+ *                                   plane per CN state so lanes (cells) coalesce
+ *   cn_obs/rep_obs uint8 [L][N]    step-1 observed states
+ *   packed params (unconstrained, see pert_layout below), float
+ */
+#ifndef PERT_HIP_H
+#define PERT_HIP_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PERT_KIND_STEP1 1   /* G1/2 cells, cn/rep observed (pert_model.py:718-774) */
+#define PERT_KIND_STEP2 2   /* S cells, cn x rep enumerated (:776-830) */
+#define PERT_KIND_STEP3 3   /* step 2 with rho, a frozen, on G1 cells (:834-896) */
+
+#define PERT_MODE_STEP   0  /* ELBO + grads + fused Adam on pi + reduction partials */
+#define PERT_MODE_GRAD   1  /* ELBO + grads; d(-ELBO)/dz_pi written to g_pi, no update */
+#define PERT_MODE_DECODE 2  /* joint argmax over (rep, cn): cn_out, rep_out */
+
+#define PERT_OK 0
+#define PERT_E_ARG 1
+#define PERT_E_UNSUPPORTED_P 2
+#define PERT_E_UNSUPPORTED_K 3
+#define PERT_E_HIP_BASE 1000
+
+#define PERT_MAX_K1 8      /* K + 1 <= 8 */
+#define PERT_MIN_P 2
+#define PERT_MAX_P 16
+#define PERT_BLOCK 256     /* cells per workgroup (4 waves x 64 lanes) */
+
+/* Offsets into the packed parameter / gradient vectors.  The shared block
+ * [0, n_shared) is replicated on every rank and its gradient is all-reduced;
+ * the cell block [n_shared, n_params) is local to the rank's cell shard. */
+typedef struct {
+  int32_t off_rho;     /* L    z_rho (unit interval)                          */
+  int32_t off_a;       /* 1    z_a   (positive)                               */
+  int32_t off_lam;     /* 1    z_lambda (interval(0.001, 0.999)), step 1      */
+  int32_t off_bstds;   /* n_libs*K1  z_beta_stds (positive)                   */
+  int32_t off_bmeans;  /* n_libs*K1  beta_means (real), step 1                */
+  int32_t n_shared;
+  int32_t off_u;       /* N    u (real)                                        */
+  int32_t off_beta;    /* K1*N betas, plane layout [k][n]                      */
+  int32_t off_tau;     /* N    z_tau (unit interval)                           */
+  int32_t n_params;
+} pert_layout;
+
+typedef struct {
+  int32_t kind, L, N, P, K1, n_libs, n_codes;
+  int32_t is_root;                 /* adds the global priors once across ranks */
+  const float* reads;
+  const float* gcf;
+  const int32_t* libs;             /* [N] library index per cell */
+  const uint16_t* eta_code;        /* steps 2/3 */
+  const float* eta_table;
+  const uint8_t* cn_obs;           /* step 1 */
+  const uint8_t* rep_obs;
+  const float* mean_reads;         /* [N] mean over bins of reads (u prior, :597) */
+  const float* ploidy;             /* [N] mean argmax eta (steps 2/3) or 2 (step 1) */
+  float lamb;                      /* steps 2/3: fixed lambda from step 1 */
+  float log1m_lam;                 /* log(1 - lamb) */
+  float sum_reads;                 /* step 1: sum of reads of this shard (d/dlam of x log lam) */
+  float a_fixed;                   /* step 3 */
+  const float* beta_means;         /* steps 2/3 fixed [n_libs][K1] */
+  const float* rho_fixed;          /* step 3 [L] constrained */
+} pert_problem;
+
+typedef struct {
+  pert_layout lay;
+  float* params;                   /* [n_params] unconstrained */
+  float* adam_m;                   /* [n_params] */
+  float* adam_v;                   /* [n_params] */
+  double* grad_shared;             /* [n_shared + 1]: d loss / d shared params, then loss (local sum) */
+  float* grad_cell;                /* [n_params - n_shared] */
+  float* z_pi;                     /* [L][P][N] steps 2/3 */
+  float* m_pi;
+  float* v_pi;
+  float* g_pi;                     /* [L][P][N] only for PERT_MODE_GRAD */
+  uint8_t* cn_out;                 /* [L][N] PERT_MODE_DECODE */
+  uint8_t* rep_out;
+  /* workspace, sized by pert_workspace_sizes() */
+  float* cell_part;
+  float* bin_part;
+  double* blk_part;
+  double* cellblk_part;
+  int32_t bins_per_tile;           /* LT; 0 = library default */
+} pert_state;
+
+typedef struct {
+  float lr, beta1, beta2, eps;
+  float step_size;                 /* lr / (1 - beta1^t)               (torch/optim/adam.py) */
+  float inv_bc2_sqrt;              /* 1 / sqrt(1 - beta2^t)                               */
+} pert_adam_hparams;
+
+/* Packed layout for (kind, L, N, K1, n_libs). */
+int pert_make_layout(int32_t L, int32_t N, int32_t K1, int32_t n_libs, pert_layout* out);
+
+/* Workspace element counts for cell_part (float), bin_part (float), blk_part (double),
+ * cellblk_part (double) at bins_per_tile (0 = default). */
+int pert_workspace_sizes(int32_t kind, int32_t L, int32_t N, int32_t K1, int32_t n_libs,
+                         int32_t bins_per_tile, int64_t* n_cell_part, int64_t* n_bin_part,
+                         int64_t* n_blk_part, int64_t* n_cellblk_part);
+
+/* Enumerated (steps 2/3) pass over every (bin, cell) of the shard.
+ * Replaces the JitTraceEnum_ELBO forward + autograd backward of pert_model.py:801 / :868,
+ * and with PERT_MODE_STEP the pi part of the Adam update; with PERT_MODE_DECODE it is
+ * infer_discrete(temperature=0) of :820-827 / :886-893. */
+int pert_enum_pass(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
+                   int32_t mode, hipStream_t stream);
+
+/* Observed (step 1) pass: JitTrace_ELBO forward + backward of pert_model.py:743. */
+int pert_obs_pass(const pert_problem* prob, pert_state* st, hipStream_t stream);
+
+/* Reductions of the pass partials + priors of the non-enumerated sites (pert_model.py:553-603)
+ * -> grad_cell (local) and grad_shared (local partial sums incl. the loss in slot n_shared). */
+int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream);
+
+/* Adam (torch.optim.Adam semantics, betas (0.8, 0.99)) on the packed params with
+ * grad_shared (already all-reduced) and grad_cell. */
+int pert_adam(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
+              hipStream_t stream);
+
+/* Test-only entry points: the per-(bin, cell) arithmetic of pert_math.h evaluated on
+ * the host (no GPU needed) or on the device, for the parity suite.  Not used by any
+ * product path. */
+int pert_selftest_nb_lgdiff_host(int64_t n, const float* d, const float* x, float* lam, float* psi);
+int pert_selftest_nb_lgdiff_device(int64_t n, const float* d, const float* x, float* lam, float* psi,
+                                   hipStream_t stream);
+int pert_selftest_enum_cellbin_host(int32_t P, int64_t n, const float* x, const float* em1,
+                                    const float* S1, const float* z, float log1m_lam,
+                                    const float* D, const float* phi, float* E, float* dirv,
+                                    float* gD, float* gt, float* gz, int32_t* argmax);
+
+const char* pert_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PERT_HIP_H */

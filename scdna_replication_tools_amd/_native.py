@@ -1,0 +1,162 @@
+"""ctypes binding of libpert_hip.so (the C ABI declared in include/pert_hip.h).
+
+There is no fallback: if the shared library is missing or fails to load, every
+product entry point raises ``NativeLibraryError``.  Build it with
+``python -m scdna_replication_tools_amd.build`` (or ``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_void_p
+
+LIB_NAME = "libpert_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+KIND_STEP1, KIND_STEP2, KIND_STEP3 = 1, 2, 3
+MODE_STEP, MODE_GRAD, MODE_DECODE = 0, 1, 2
+MAX_K1 = 8
+MIN_P, MAX_P = 2, 16
+BLOCK = 256
+
+# every symbol include/pert_hip.h declares
+EXPORTED_SYMBOLS = (
+    "pert_make_layout", "pert_workspace_sizes", "pert_enum_pass", "pert_obs_pass",
+    "pert_finalize", "pert_adam", "pert_selftest_nb_lgdiff_host",
+    "pert_selftest_nb_lgdiff_device", "pert_selftest_enum_cellbin_host", "pert_version",
+)
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class PertLayout(ctypes.Structure):
+    _fields_ = [(n, c_int32) for n in ("off_rho", "off_a", "off_lam", "off_bstds", "off_bmeans",
+                                       "n_shared", "off_u", "off_beta", "off_tau", "n_params")]
+
+
+class PertProblem(ctypes.Structure):
+    _fields_ = [
+        ("kind", c_int32), ("L", c_int32), ("N", c_int32), ("P", c_int32), ("K1", c_int32),
+        ("n_libs", c_int32), ("n_codes", c_int32), ("is_root", c_int32),
+        ("reads", c_void_p), ("gcf", c_void_p), ("libs", c_void_p), ("eta_code", c_void_p),
+        ("eta_table", c_void_p), ("cn_obs", c_void_p), ("rep_obs", c_void_p),
+        ("mean_reads", c_void_p), ("ploidy", c_void_p),
+        ("lamb", c_float), ("log1m_lam", c_float), ("sum_reads", c_float), ("a_fixed", c_float),
+        ("beta_means", c_void_p), ("rho_fixed", c_void_p),
+    ]
+
+
+class PertState(ctypes.Structure):
+    _fields_ = [
+        ("lay", PertLayout),
+        ("params", c_void_p), ("adam_m", c_void_p), ("adam_v", c_void_p),
+        ("grad_shared", c_void_p), ("grad_cell", c_void_p),
+        ("z_pi", c_void_p), ("m_pi", c_void_p), ("v_pi", c_void_p), ("g_pi", c_void_p),
+        ("cn_out", c_void_p), ("rep_out", c_void_p),
+        ("cell_part", c_void_p), ("bin_part", c_void_p), ("blk_part", c_void_p),
+        ("cellblk_part", c_void_p),
+        ("bins_per_tile", c_int32),
+    ]
+
+
+class PertAdamHparams(ctypes.Structure):
+    _fields_ = [(n, c_float) for n in ("lr", "beta1", "beta2", "eps", "step_size", "inv_bc2_sqrt")]
+
+
+_lib = None
+
+
+def lib():
+    """Load libpert_hip.so once; raise loudly if it is absent or incomplete."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    # torch first: its bundled libamdhip64 (soname libamdhip64.so.7) must be the one HIP
+    # runtime of the process, so our kernels and torch's allocations share a context.
+    import torch  # noqa: F401
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryError(
+            "{} not found: the PERT HIP extension is not built (run "
+            "`python -m scdna_replication_tools_amd.build`). There is no CPU fallback.".format(LIB_PATH))
+    try:
+        handle = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover
+        raise NativeLibraryError("failed to load {}: {}".format(LIB_PATH, e))
+    missing = [s for s in EXPORTED_SYMBOLS if not hasattr(handle, s)]
+    if missing:
+        raise NativeLibraryError("{} lacks symbols {}".format(LIB_PATH, missing))
+    i32, i64 = c_int32, c_int64
+    fp = POINTER(c_float)
+    handle.pert_make_layout.argtypes = [i32, i32, i32, i32, POINTER(PertLayout)]
+    handle.pert_workspace_sizes.argtypes = [i32, i32, i32, i32, i32, i32, POINTER(i64), POINTER(i64),
+                                            POINTER(i64), POINTER(i64)]
+    handle.pert_enum_pass.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams),
+                                      i32, c_void_p]
+    handle.pert_obs_pass.argtypes = [POINTER(PertProblem), POINTER(PertState), c_void_p]
+    handle.pert_finalize.argtypes = [POINTER(PertProblem), POINTER(PertState), c_void_p]
+    handle.pert_adam.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams), c_void_p]
+    handle.pert_selftest_nb_lgdiff_host.argtypes = [i64, fp, fp, fp, fp]
+    handle.pert_selftest_nb_lgdiff_device.argtypes = [i64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+    handle.pert_selftest_enum_cellbin_host.argtypes = [i32, i64, fp, fp, fp, fp, c_float, fp, fp, fp, fp,
+                                                       fp, fp, fp, POINTER(i32)]
+    handle.pert_version.restype = c_char_p
+    for name in EXPORTED_SYMBOLS:
+        if name != "pert_version":
+            getattr(handle, name).restype = c_int32
+    _lib = handle
+    return _lib
+
+
+def check(code: int, what: str):
+    if code != 0:
+        if code >= 1000:
+            raise RuntimeError("{} failed: HIP error {}".format(what, code - 1000))
+        raise ValueError("{} failed: status {}".format(what, code))
+
+
+def make_layout(L: int, N: int, K1: int, n_libs: int) -> PertLayout:
+    lay = PertLayout()
+    check(lib().pert_make_layout(L, N, K1, n_libs, ctypes.byref(lay)), "pert_make_layout")
+    return lay
+
+
+def workspace_sizes(kind: int, L: int, N: int, K1: int, n_libs: int, bins_per_tile: int = 0):
+    out = [c_int64() for _ in range(4)]
+    check(lib().pert_workspace_sizes(kind, L, N, K1, n_libs, bins_per_tile, *[ctypes.byref(o) for o in out]),
+          "pert_workspace_sizes")
+    return tuple(int(o.value) for o in out)
+
+
+def _fptr(a):
+    return a.ctypes.data_as(POINTER(c_float))
+
+
+def selftest_nb_lgdiff_host(d, x):
+    """Host evaluation of pert_math.h nb_lgdiff (test-only)."""
+    import numpy as np
+    d = np.ascontiguousarray(d, dtype=np.float32)
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    lam = np.empty_like(d)
+    psi = np.empty_like(d)
+    check(lib().pert_selftest_nb_lgdiff_host(d.size, _fptr(d), _fptr(x), _fptr(lam), _fptr(psi)),
+          "pert_selftest_nb_lgdiff_host")
+    return lam, psi
+
+
+def selftest_enum_cellbin_host(P, x, em1, S1, z, log1m_lam, D, phi):
+    """Host evaluation of pert_math.h enum_cellbin (test-only)."""
+    import numpy as np
+    f = lambda a: np.ascontiguousarray(a, dtype=np.float32)
+    x, em1, S1, z, D, phi = map(f, (x, em1, S1, z, D, phi))
+    n = x.size
+    E, dirv, gD, gt = (np.empty(n, np.float32) for _ in range(4))
+    gz = np.empty((n, P), np.float32)
+    am = np.empty(n, np.int32)
+    check(lib().pert_selftest_enum_cellbin_host(P, n, _fptr(x), _fptr(em1), _fptr(S1), _fptr(z),
+                                                float(log1m_lam), _fptr(D), _fptr(phi), _fptr(E),
+                                                _fptr(dirv), _fptr(gD), _fptr(gt), _fptr(gz),
+                                                am.ctypes.data_as(POINTER(c_int32))),
+          "pert_selftest_enum_cellbin_host")
+    return dict(E=E, dirv=dirv, gD=gD, gt=gt, gz=gz, argmax=am)

@@ -1,0 +1,699 @@
+// pert_kernels.hip -- gfx950 kernels of the PERT SVI hot path + the C ABI of include/pert_hip.h.
+//
+// One SVI step of reference pert_model.py (svi_s.step at :801, svi.step at :743,
+// svi_s2.step at :868) becomes:
+//   enum_kernel / obs_kernel   one pass over every (bin, cell): forward, analytic backward,
+//                              fused Adam on the (L, P, N) pi logits, reduction partials
+//   finalize_kernel            per-cell sums + u / betas / tau priors (:589-603),
+//                              per-bin sums for rho (:572-574)
+//   scalar_kernel              global sums (loss, a, beta_stds, lambda, beta_means)
+//   adam_kernel                Adam on the packed non-pi params
+// All reductions are fixed-order (no float atomics), so a rerun is bit-identical.
+//
+// Work decomposition: workgroup = 256 cells (4 waves, one cell per lane) x LT bins.
+// Lanes walk their bins in order; per-cell partial sums stay in registers, per-bin
+// sums are wave shuffles + LDS.  Every HBM access of the (L, N) / (L, P, N) tensors is a
+// 256-byte contiguous wave access (cells are the fastest axis).
+
+#include "../../include/pert_hip.h"
+#include "pert_math.h"
+
+#include <math.h>
+#include <stddef.h>
+
+namespace {
+
+using namespace pert;
+
+constexpr int kBlock = PERT_BLOCK;
+constexpr int kWaves = kBlock / 64;
+constexpr int kDefaultLT = 32;
+constexpr int kMaxLT = 64;
+constexpr int kBlkSlots = 4;      // loss, d/da, sum delta, sum gdd (step 1)
+constexpr float kHalfLog2PiF = 0.918938533204672742f;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Block-wide fixed-order sum; every thread gets the result.
+__device__ __forceinline__ double block_sum_d(double v, double* sm) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = wave_sum_d(v);
+  __syncthreads();
+  if (lane == 0) sm[wave] = v;
+  __syncthreads();
+  double t = 0.0;
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) t += sm[w];
+  return t;
+}
+
+__device__ __forceinline__ float gamma_lp_a(float a) {
+  // Gamma(2, 0.2).log_prob(a) = xlogy(2, 0.2) + xlogy(1, a) - 0.2 a - lgamma(2)   (pert_model.py:553)
+  return 2.0f * logf(0.2f) + logf(a) - 0.2f * a;
+}
+
+// ------------------------------------------------------------------------------------------
+// Enumerated pass (steps 2/3).  MODE: PERT_MODE_STEP / PERT_MODE_GRAD / PERT_MODE_DECODE.
+template <int P, int MODE>
+__global__ void __launch_bounds__(kBlock) enum_kernel(pert_problem pr, pert_state st,
+                                                       pert_adam_hparams hp) {
+  constexpr bool kDecode = MODE == PERT_MODE_DECODE;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int N = pr.N, K1 = pr.K1;
+  const int n = blockIdx.x * kBlock + tid;
+  const bool valid = n < N;
+  const int LT = st.bins_per_tile;
+  const int l0 = blockIdx.y * LT;
+  const int l1 = min(pr.L, l0 + LT);
+  const bool frozen = pr.kind == PERT_KIND_STEP3;
+  const pert_layout lay = st.lay;
+
+  __shared__ float s_bin[kWaves][kMaxLT];
+  __shared__ double s_red[kWaves];
+
+  const float a_val = frozen ? pr.a_fixed : fexp(st.params[lay.off_a]);
+  const float c0 = (1.0f - pr.lamb) / pr.lamb;
+
+  float u = 0.0f, tau = 0.5f;
+  float beta[PERT_MAX_K1];
+#pragma unroll
+  for (int k = 0; k < PERT_MAX_K1; ++k) beta[k] = 0.0f;
+  if (valid) {
+    u = st.params[lay.off_u + n];
+#pragma unroll
+    for (int k = 0; k < PERT_MAX_K1; ++k)
+      if (k < K1) beta[k] = st.params[lay.off_beta + k * N + n];
+    float dm;
+    tau = clipped_sigmoid(st.params[lay.off_tau + n], &dm);
+  }
+  const float ucc = u * c0;
+
+  float acc[PERT_MAX_K1];
+#pragma unroll
+  for (int k = 0; k < PERT_MAX_K1; ++k) acc[k] = 0.0f;
+  float accT = 0.0f, loss = 0.0f, ga = 0.0f;
+
+  for (int l = l0; l < l1; ++l) {
+    float rho;
+    if (frozen) {
+      rho = pr.rho_fixed[l];
+    } else {
+      float dm;
+      rho = clipped_sigmoid(st.params[lay.off_rho + l], &dm);
+    }
+    float g[PERT_MAX_K1];
+#pragma unroll
+    for (int k = 0; k < PERT_MAX_K1; ++k) g[k] = (k < K1) ? pr.gcf[l * K1 + k] : 0.0f;
+    float gt = 0.0f;
+    if (valid) {
+      const size_t ln = (size_t)l * N + n;
+      const float x = pr.reads[ln];
+      const float invx = x > 0.0f ? 1.0f / x : 0.0f;
+      float dot = 0.0f;
+#pragma unroll
+      for (int k = 0; k < PERT_MAX_K1; ++k) dot += beta[k] * g[k];
+      const float omega = fexp(dot);                         // pert_model.py:633
+      const float D = ucc * omega;                           // :636-640 (delta = chi D)
+      const float t = tau - rho;                             // :616
+      const float phi = 1.0f / (1.0f + fexp(-a_val * t));    // :619
+      const float* row = pr.eta_table + (size_t)pr.eta_code[ln] * (P + 1);
+      float em1[P], z[P];
+#pragma unroll
+      for (int k = 0; k < P; ++k) em1[k] = row[k];
+      const float S1 = row[P];
+      const size_t plane = (size_t)l * P * N + n;
+#pragma unroll
+      for (int k = 0; k < P; ++k) z[k] = st.z_pi[plane + (size_t)k * N];
+      EnumOut<P> o;
+      enum_cellbin<P, !kDecode, kDecode>(x, invx, em1, S1, z, pr.log1m_lam, D, phi, o);
+      if (kDecode) {
+        st.cn_out[ln] = (uint8_t)(o.argmax % P);
+        st.rep_out[ln] = (uint8_t)(o.argmax / P);
+      } else {
+        loss += o.E + o.dirv;
+        gt = o.gt;
+        accT += a_val * o.gt;
+        ga += t * o.gt;
+        const float ge = o.gD * omega;
+#pragma unroll
+        for (int k = 0; k < PERT_MAX_K1; ++k) acc[k] += ge * g[k];
+        if (MODE == PERT_MODE_STEP) {
+#pragma unroll
+          for (int k = 0; k < P; ++k) {
+            const size_t idx = plane + (size_t)k * N;
+            const float gl = -o.gz[k];                      // d(-ELBO)/dz
+            float mm = st.m_pi[idx], vv = st.v_pi[idx];
+            mm = hp.beta1 * mm + (1.0f - hp.beta1) * gl;
+            vv = hp.beta2 * vv + (1.0f - hp.beta2) * gl * gl;
+            const float denom = sqrtf(vv) * hp.inv_bc2_sqrt + hp.eps;
+            st.z_pi[idx] = z[k] - hp.step_size * mm / denom;
+            st.m_pi[idx] = mm;
+            st.v_pi[idx] = vv;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < P; ++k) st.g_pi[plane + (size_t)k * N] = -o.gz[k];
+        }
+      }
+    }
+    if (!kDecode && !frozen) {
+      const float ws = wave_sum(gt);
+      if (lane == 0) s_bin[wave][l - l0] = ws;
+    }
+  }
+  if (kDecode) return;
+
+  __syncthreads();
+  if (!frozen && tid < l1 - l0) {
+    float s = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) s += s_bin[w][tid];
+    st.bin_part[(size_t)blockIdx.x * pr.L + l0 + tid] = s;
+  }
+  if (valid) {
+    float* cp = st.cell_part + (size_t)blockIdx.y * (K1 + 1) * N + n;
+#pragma unroll
+    for (int k = 0; k < PERT_MAX_K1; ++k)
+      if (k < K1) cp[(size_t)k * N] = acc[k];
+    cp[(size_t)K1 * N] = accT;
+  }
+  const double bl = block_sum_d((double)loss, s_red);
+  const double bga = block_sum_d((double)ga, s_red);
+  if (tid == 0) {
+    double* bp = st.blk_part + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlkSlots;
+    bp[0] = bl;
+    bp[1] = bga;
+    bp[2] = 0.0;
+    bp[3] = 0.0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Observed pass (step 1): cn, rep conditioned (pert_model.py:724-729).
+__global__ void __launch_bounds__(kBlock) obs_kernel(pert_problem pr, pert_state st) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int N = pr.N, K1 = pr.K1;
+  const int n = blockIdx.x * kBlock + tid;
+  const bool valid = n < N;
+  const int LT = st.bins_per_tile;
+  const int l0 = blockIdx.y * LT;
+  const int l1 = min(pr.L, l0 + LT);
+  const pert_layout lay = st.lay;
+
+  __shared__ float s_bin[kWaves][kMaxLT];
+  __shared__ double s_red[kWaves];
+
+  const float a_val = fexp(st.params[lay.off_a]);
+  float dml;
+  const float lam = 0.001f + 0.998f * clipped_sigmoid(st.params[lay.off_lam], &dml);
+  const float c0 = (1.0f - lam) / lam;
+  const float log1m_lam = logf(1.0f - lam);
+
+  float u = 0.0f, tau = 0.5f;
+  float beta[PERT_MAX_K1];
+#pragma unroll
+  for (int k = 0; k < PERT_MAX_K1; ++k) beta[k] = 0.0f;
+  if (valid) {
+    u = st.params[lay.off_u + n];
+#pragma unroll
+    for (int k = 0; k < PERT_MAX_K1; ++k)
+      if (k < K1) beta[k] = st.params[lay.off_beta + k * N + n];
+    float dm;
+    tau = clipped_sigmoid(st.params[lay.off_tau + n], &dm);
+  }
+  const float ucc = u * c0;
+  float acc[PERT_MAX_K1];
+#pragma unroll
+  for (int k = 0; k < PERT_MAX_K1; ++k) acc[k] = 0.0f;
+  float accT = 0.0f, loss = 0.0f, ga = 0.0f, dsum = 0.0f, gdd = 0.0f;
+
+  for (int l = l0; l < l1; ++l) {
+    float dm;
+    const float rho = clipped_sigmoid(st.params[lay.off_rho + l], &dm);
+    float g[PERT_MAX_K1];
+#pragma unroll
+    for (int k = 0; k < PERT_MAX_K1; ++k) g[k] = (k < K1) ? pr.gcf[l * K1 + k] : 0.0f;
+    float gt = 0.0f;
+    if (valid) {
+      const size_t ln = (size_t)l * N + n;
+      const float x = pr.reads[ln];
+      const float invx = x > 0.0f ? 1.0f / x : 0.0f;
+      float dot = 0.0f;
+#pragma unroll
+      for (int k = 0; k < PERT_MAX_K1; ++k) dot += beta[k] * g[k];
+      const float omega = fexp(dot);
+      const float D = ucc * omega;
+      const float t = tau - rho;
+      const float phi = 1.0f / (1.0f + fexp(-a_val * t));
+      ObsOut o;
+      obs_cellbin(x, invx, (float)pr.cn_obs[ln], (float)pr.rep_obs[ln], log1m_lam, D, phi, o);
+      loss += o.ll;
+      gt = o.gt;
+      accT += a_val * o.gt;
+      ga += t * o.gt;
+      dsum += o.dsum;
+      gdd += o.gdd;
+      const float ge = o.gD * omega;
+#pragma unroll
+      for (int k = 0; k < PERT_MAX_K1; ++k) acc[k] += ge * g[k];
+    }
+    const float ws = wave_sum(gt);
+    if (lane == 0) s_bin[wave][l - l0] = ws;
+  }
+  __syncthreads();
+  if (tid < l1 - l0) {
+    float s = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) s += s_bin[w][tid];
+    st.bin_part[(size_t)blockIdx.x * pr.L + l0 + tid] = s;
+  }
+  if (valid) {
+    float* cp = st.cell_part + (size_t)blockIdx.y * (K1 + 1) * N + n;
+#pragma unroll
+    for (int k = 0; k < PERT_MAX_K1; ++k)
+      if (k < K1) cp[(size_t)k * N] = acc[k];
+    cp[(size_t)K1 * N] = accT;
+  }
+  const double bl = block_sum_d((double)loss, s_red);
+  const double bga = block_sum_d((double)ga, s_red);
+  const double bds = block_sum_d((double)dsum, s_red);
+  const double bgd = block_sum_d((double)gdd, s_red);
+  if (tid == 0) {
+    double* bp = st.blk_part + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlkSlots;
+    bp[0] = bl;
+    bp[1] = bga;
+    bp[2] = bds;
+    bp[3] = bgd;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-cell and per-bin reductions + priors of the non-enumerated sites.
+// Blocks [0, n_cblk) handle 256 cells each; blocks [n_cblk, n_cblk + n_lblk) 256 bins each.
+__global__ void __launch_bounds__(kBlock) finalize_kernel(pert_problem pr, pert_state st,
+                                                          int n_cblk, int n_bt, int n_ct) {
+  const int tid = threadIdx.x;
+  const int N = pr.N, K1 = pr.K1, L = pr.L, nl = pr.n_libs;
+  const pert_layout lay = st.lay;
+  const bool step1 = pr.kind == PERT_KIND_STEP1;
+  __shared__ double s_red[kWaves];
+
+  if ((int)blockIdx.x >= n_cblk) {
+    // ---- per-bin: d(-ELBO)/dz_rho   (rho ~ Beta(1,1) has zero log density, :574)
+    const int l = (blockIdx.x - n_cblk) * kBlock + tid;
+    if (l >= L) return;
+    if (pr.kind == PERT_KIND_STEP3) { st.grad_shared[lay.off_rho + l] = 0.0; return; }
+    double s = 0.0;
+    for (int ct = 0; ct < n_ct; ++ct) s += (double)st.bin_part[(size_t)ct * L + l];
+    const float a_val = fexp(st.params[lay.off_a]);
+    float dmask;
+    clipped_sigmoid(st.params[lay.off_rho + l], &dmask);
+    // dE/drho = -a sum_n gt ;  loss gradient = +a sum gt * drho/dz
+    st.grad_shared[lay.off_rho + l] = (double)a_val * s * (double)dmask;
+    return;
+  }
+
+  // ---- per-cell
+  const int n = blockIdx.x * kBlock + tid;
+  const bool valid = n < N;
+  float lam = pr.lamb;
+  if (step1) {
+    float dml;
+    lam = 0.001f + 0.998f * clipped_sigmoid(st.params[lay.off_lam], &dml);
+  }
+  const float c0 = (1.0f - lam) / lam;
+  double lp = 0.0;
+  float dzbs[PERT_MAX_K1], dbm[PERT_MAX_K1];
+  int lib = 0;
+#pragma unroll
+  for (int k = 0; k < PERT_MAX_K1; ++k) { dzbs[k] = 0.0f; dbm[k] = 0.0f; }
+  if (valid) {
+    double A[PERT_MAX_K1], T = 0.0;
+#pragma unroll
+    for (int k = 0; k < PERT_MAX_K1; ++k) A[k] = 0.0;
+    for (int bt = 0; bt < n_bt; ++bt) {
+      const float* cp = st.cell_part + (size_t)bt * (K1 + 1) * N + n;
+#pragma unroll
+      for (int k = 0; k < PERT_MAX_K1; ++k)
+        if (k < K1) A[k] += (double)cp[(size_t)k * N];
+      T += (double)cp[(size_t)K1 * N];
+    }
+    const float u = st.params[lay.off_u + n];
+    float dtau_dz;
+    const float tau = clipped_sigmoid(st.params[lay.off_tau + n], &dtau_dz);
+    lib = pr.libs[n];
+    // data terms: dE/du = c0 sum_l gD omega (intercept column of gcf is 1), dE/dbeta_k = u c0 sum gD omega g_k
+    float dU = c0 * (float)A[K1 - 1];
+    float dTau = (float)T;
+    float dB[PERT_MAX_K1];
+#pragma unroll
+    for (int k = 0; k < PERT_MAX_K1; ++k) dB[k] = (k < K1) ? u * c0 * (float)A[k] : 0.0f;
+
+    // u ~ Normal(mu, mu/10), mu = mean(x) / ((1 + tau) ploidy)   (:597-600)
+    const float mu = pr.mean_reads[n] / ((1.0f + tau) * pr.ploidy[n]);
+    const float sg = mu / 10.0f;
+    const float w = (u - mu) / sg;
+    lp += (double)(-0.5f * w * w - logf(sg) - kHalfLog2PiF);
+    dU += -w / sg;
+    const float dmu = w / sg + 0.1f * w * w / sg - 0.1f / sg;
+    dTau += dmu * (-mu / (1.0f + tau));
+
+    // betas ~ Normal(beta_means[lib], beta_stds[lib]).to_event(1)   (:603)
+#pragma unroll
+    for (int k = 0; k < PERT_MAX_K1; ++k) {
+      if (k >= K1) continue;
+      const float bsd = fexp(st.params[lay.off_bstds + lib * K1 + k]);
+      const float bmn = step1 ? st.params[lay.off_bmeans + lib * K1 + k] : pr.beta_means[lib * K1 + k];
+      const float b = st.params[lay.off_beta + k * N + n];
+      const float wk = (b - bmn) / bsd;
+      lp += (double)(-0.5f * wk * wk - logf(bsd) - kHalfLog2PiF);
+      dB[k] += -wk / bsd;
+      dzbs[k] = wk * wk - 1.0f;          // d/dz_bstds (z = log beta_stds)
+      dbm[k] = wk / bsd;                 // d/dbeta_means (step 1)
+    }
+    if (step1) {
+      // tau ~ Beta(1.5, 1.5)  (:585): 0.5 log tau + 0.5 log(1-tau) + lgamma(3) - 2 lgamma(1.5)
+      lp += (double)(0.5f * logf(tau) + 0.5f * logf(1.0f - tau) + 0.69314718055994531f
+                     - 2.0f * (-0.12078223763524522f));
+      dTau += 0.5f / tau - 0.5f / (1.0f - tau);
+    }
+    float* gc = st.grad_cell - lay.n_shared;
+    gc[lay.off_u + n] = -dU;
+#pragma unroll
+    for (int k = 0; k < PERT_MAX_K1; ++k)
+      if (k < K1) gc[lay.off_beta + k * N + n] = -dB[k];
+    gc[lay.off_tau + n] = -dTau * dtau_dz;
+  }
+  // per-library sums for beta_stds (and beta_means in step 1), plus the prior log densities
+  const int nslot = 2 * nl * K1 + 1;
+  double* out = st.cellblk_part + (size_t)blockIdx.x * nslot;
+  for (int li = 0; li < nl; ++li) {
+    for (int k = 0; k < K1; ++k) {
+      const bool mine = valid && lib == li;
+      const double s1 = block_sum_d(mine ? (double)dzbs[k] : 0.0, s_red);
+      const double s2 = step1 ? block_sum_d(mine ? (double)dbm[k] : 0.0, s_red) : 0.0;
+      if (tid == 0) {
+        out[li * K1 + k] = s1;
+        out[nl * K1 + li * K1 + k] = s2;
+      }
+    }
+  }
+  const double slp = block_sum_d(lp, s_red);
+  if (tid == 0) out[2 * nl * K1] = slp;
+}
+
+// Global sums: one workgroup, fixed order.
+__global__ void __launch_bounds__(kBlock) scalar_kernel(pert_problem pr, pert_state st, int n_blk,
+                                                        int n_cblk) {
+  const int tid = threadIdx.x;
+  const int K1 = pr.K1, nl = pr.n_libs;
+  const pert_layout lay = st.lay;
+  const int kind = pr.kind;
+  __shared__ double s_red[kWaves];
+  double v[kBlkSlots] = {0.0, 0.0, 0.0, 0.0};
+  for (int b = tid; b < n_blk; b += kBlock)
+#pragma unroll
+    for (int j = 0; j < kBlkSlots; ++j) v[j] += st.blk_part[(size_t)b * kBlkSlots + j];
+  double tot[kBlkSlots];
+#pragma unroll
+  for (int j = 0; j < kBlkSlots; ++j) tot[j] = block_sum_d(v[j], s_red);
+
+  const int nslot = 2 * nl * K1 + 1;
+  double elbo = tot[0];
+  // cell-block partials
+  for (int s = 0; s < nslot; ++s) {
+    double acc = 0.0;
+    for (int b = tid; b < n_cblk; b += kBlock) acc += st.cellblk_part[(size_t)b * nslot + s];
+    const double S = block_sum_d(acc, s_red);
+    if (s < nl * K1) {
+      if (tid == 0) st.grad_shared[lay.off_bstds + s] = -S;
+    } else if (s < 2 * nl * K1) {
+      if (kind == PERT_KIND_STEP1) {
+        const int j = s - nl * K1;
+        const double bm = st.params[lay.off_bmeans + j];
+        // beta_means ~ N(0, 1) (:560): prior gradient -bm added once (root)
+        if (tid == 0) st.grad_shared[lay.off_bmeans + j] = -(S + (pr.is_root ? -bm : 0.0));
+      } else if (tid == 0) {
+        st.grad_shared[lay.off_bmeans + (s - nl * K1)] = 0.0;
+      }
+    } else {
+      elbo += S;
+    }
+  }
+  if (tid != 0) return;
+  // global sites
+  if (kind != PERT_KIND_STEP3) {
+    const double a = exp((double)st.params[lay.off_a]);
+    double dza = a * tot[1];                               // dE/dz_a = a dE/da (data part)
+    if (pr.is_root) {
+      dza += 1.0 - 0.2 * a;                                // Gamma(2, 0.2) prior through a = exp(z)
+      elbo += (double)gamma_lp_a((float)a);
+    }
+    st.grad_shared[lay.off_a] = -dza;
+  } else {
+    st.grad_shared[lay.off_a] = 0.0;
+    if (pr.is_root) elbo += (double)gamma_lp_a(pr.a_fixed);   // observed a (:847)
+  }
+  if (kind == PERT_KIND_STEP1) {
+    float dml;
+    const float s = clipped_sigmoid(st.params[lay.off_lam], &dml);
+    const double lam = 0.001 + 0.998 * (double)s;
+    // d/dlam of sum[delta log(1-lam) + x log lam] with delta = chi u omega (1-lam)/lam
+    const double dlam = -tot[2] / (1.0 - lam) + (double)pr.sum_reads / lam - tot[3] / (lam * (1.0 - lam));
+    st.grad_shared[lay.off_lam] = -dlam * 0.998 * (double)dml;
+    elbo += (double)pr.sum_reads * log(lam);
+    if (pr.is_root) {
+      double bmlp = 0.0;
+      for (int j = 0; j < nl * K1; ++j) {
+        const double bm = st.params[lay.off_bmeans + j];
+        bmlp += -0.5 * bm * bm - 0.91893853320467274;
+      }
+      elbo += bmlp;
+    }
+  } else {
+    st.grad_shared[lay.off_lam] = 0.0;
+    if (pr.is_root) {                                      // observed beta_means (:785)
+      double bmlp = 0.0;
+      for (int j = 0; j < nl * K1; ++j) {
+        const double bm = pr.beta_means[j];
+        bmlp += -0.5 * bm * bm - 0.91893853320467274;
+      }
+      elbo += bmlp;
+    }
+  }
+  st.grad_shared[lay.n_shared] = -elbo;                     // local loss (host adds constants)
+}
+
+// Adam on the packed params (torch.optim.Adam, pyro.optim.Adam wrapper; one state per param).
+__global__ void __launch_bounds__(kBlock) adam_kernel(pert_problem pr, pert_state st,
+                                                      pert_adam_hparams hp) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  const pert_layout lay = st.lay;
+  if (i >= lay.n_params) return;
+  const int kind = pr.kind;
+  bool active = true;
+  if (i < lay.off_a + 1 && kind == PERT_KIND_STEP3) active = false;                   // rho, a
+  if (i >= lay.off_lam && i < lay.off_lam + 1 && kind != PERT_KIND_STEP1) active = false;
+  if (i >= lay.off_bmeans && i < lay.n_shared && kind != PERT_KIND_STEP1) active = false;
+  if (!active) return;
+  const float g = i < lay.n_shared ? (float)st.grad_shared[i] : st.grad_cell[i - lay.n_shared];
+  float mm = st.adam_m[i], vv = st.adam_v[i];
+  mm = hp.beta1 * mm + (1.0f - hp.beta1) * g;
+  vv = hp.beta2 * vv + (1.0f - hp.beta2) * g * g;
+  const float denom = sqrtf(vv) * hp.inv_bc2_sqrt + hp.eps;
+  st.params[i] -= hp.step_size * mm / denom;
+  st.adam_m[i] = mm;
+  st.adam_v[i] = vv;
+}
+
+// Device self-test of nb_lgdiff (accuracy of the special functions on gfx950).
+__global__ void nb_selftest_kernel(int64_t n, const float* d, const float* x, float* lam, float* psi) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float xi = x[i];
+  float l, p;
+  nb_lgdiff(d[i], xi, xi > 0.0f ? 1.0f / xi : 0.0f, l, p);
+  lam[i] = l;
+  psi[i] = p;
+}
+
+int hip_status(hipError_t e) { return e == hipSuccess ? PERT_OK : PERT_E_HIP_BASE + (int)e; }
+
+int tile_bins(const pert_state* st) {
+  int lt = st->bins_per_tile > 0 ? st->bins_per_tile : kDefaultLT;
+  return lt > kMaxLT ? kMaxLT : lt;
+}
+
+bool problem_ok(const pert_problem* p) {
+  return p && p->L > 0 && p->N > 0 && p->K1 >= 1 && p->K1 <= PERT_MAX_K1 && p->n_libs >= 1 &&
+         p->P >= PERT_MIN_P && p->P <= PERT_MAX_P && p->reads && p->gcf && p->libs && p->mean_reads &&
+         p->ploidy;
+}
+
+template <int MODE>
+int launch_enum_mode(int P, dim3 grid, const pert_problem& pr, const pert_state& st,
+                     const pert_adam_hparams& hp, hipStream_t s) {
+  switch (P) {
+#define PERT_CASE(PP) \
+  case PP: hipLaunchKernelGGL((enum_kernel<PP, MODE>), grid, dim3(kBlock), 0, s, pr, st, hp); break;
+    PERT_CASE(2) PERT_CASE(3) PERT_CASE(4) PERT_CASE(5) PERT_CASE(6) PERT_CASE(7) PERT_CASE(8)
+    PERT_CASE(9) PERT_CASE(10) PERT_CASE(11) PERT_CASE(12) PERT_CASE(13) PERT_CASE(14)
+    PERT_CASE(15) PERT_CASE(16)
+#undef PERT_CASE
+    default: return PERT_E_UNSUPPORTED_P;
+  }
+  return hip_status(hipGetLastError());
+}
+
+template <int P>
+int selftest_enum_host(int64_t n, const float* x, const float* em1, const float* S1, const float* z,
+                       float log1m_lam, const float* D, const float* phi, float* E, float* dirv,
+                       float* gD, float* gt, float* gz, int32_t* amax) {
+  for (int64_t i = 0; i < n; ++i) {
+    float e[P], zz[P];
+    for (int k = 0; k < P; ++k) { e[k] = em1[i * P + k]; zz[k] = z[i * P + k]; }
+    EnumOut<P> o;
+    const float xi = x[i];
+    enum_cellbin<P, true, true>(xi, xi > 0.0f ? 1.0f / xi : 0.0f, e, S1[i], zz, log1m_lam, D[i], phi[i], o);
+    E[i] = o.E; dirv[i] = o.dirv; gD[i] = o.gD; gt[i] = o.gt; amax[i] = o.argmax;
+    for (int k = 0; k < P; ++k) gz[i * P + k] = o.gz[k];
+  }
+  return PERT_OK;
+}
+
+}  // namespace
+
+// ============================================================================ C ABI
+extern "C" {
+
+const char* pert_version(void) { return "pert_hip 0.1 gfx950"; }
+
+int pert_make_layout(int32_t L, int32_t N, int32_t K1, int32_t n_libs, pert_layout* o) {
+  if (!o || L <= 0 || N <= 0 || K1 < 1 || K1 > PERT_MAX_K1 || n_libs < 1) return PERT_E_ARG;
+  o->off_rho = 0;
+  o->off_a = L;
+  o->off_lam = L + 1;
+  o->off_bstds = L + 2;
+  o->off_bmeans = L + 2 + n_libs * K1;
+  o->n_shared = L + 2 + 2 * n_libs * K1;
+  o->off_u = o->n_shared;
+  o->off_beta = o->off_u + N;
+  o->off_tau = o->off_beta + K1 * N;
+  o->n_params = o->off_tau + N;
+  return PERT_OK;
+}
+
+int pert_workspace_sizes(int32_t kind, int32_t L, int32_t N, int32_t K1, int32_t n_libs,
+                         int32_t bins_per_tile, int64_t* n_cell_part, int64_t* n_bin_part,
+                         int64_t* n_blk_part, int64_t* n_cellblk_part) {
+  (void)kind;
+  if (L <= 0 || N <= 0 || K1 < 1 || K1 > PERT_MAX_K1 || n_libs < 1) return PERT_E_ARG;
+  pert_state tmp;
+  tmp.bins_per_tile = bins_per_tile;
+  const int lt = tile_bins(&tmp);
+  const int64_t n_bt = (L + lt - 1) / lt, n_ct = (N + kBlock - 1) / kBlock;
+  if (n_cell_part) *n_cell_part = n_bt * (K1 + 1) * (int64_t)N;
+  if (n_bin_part) *n_bin_part = n_ct * (int64_t)L;
+  if (n_blk_part) *n_blk_part = n_bt * n_ct * kBlkSlots;
+  if (n_cellblk_part) *n_cellblk_part = n_ct * (2 * (int64_t)n_libs * K1 + 1);
+  return PERT_OK;
+}
+
+int pert_enum_pass(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
+                   int32_t mode, hipStream_t stream) {
+  if (!problem_ok(prob) || !st || !hp) return PERT_E_ARG;
+  if (prob->kind != PERT_KIND_STEP2 && prob->kind != PERT_KIND_STEP3) return PERT_E_ARG;
+  if (!prob->eta_code || !prob->eta_table || prob->n_codes < 1 || !st->z_pi) return PERT_E_ARG;
+  if (prob->kind == PERT_KIND_STEP3 && !prob->rho_fixed) return PERT_E_ARG;
+  if (mode == PERT_MODE_STEP && (!st->m_pi || !st->v_pi)) return PERT_E_ARG;
+  if (mode == PERT_MODE_GRAD && !st->g_pi) return PERT_E_ARG;
+  if (mode == PERT_MODE_DECODE && (!st->cn_out || !st->rep_out)) return PERT_E_ARG;
+  if (mode != PERT_MODE_DECODE &&
+      (!st->cell_part || !st->bin_part || !st->blk_part || !st->params))
+    return PERT_E_ARG;
+  pert_state s2 = *st;
+  s2.bins_per_tile = tile_bins(st);
+  const dim3 grid((prob->N + kBlock - 1) / kBlock, (prob->L + s2.bins_per_tile - 1) / s2.bins_per_tile);
+  switch (mode) {
+    case PERT_MODE_STEP: return launch_enum_mode<PERT_MODE_STEP>(prob->P, grid, *prob, s2, *hp, stream);
+    case PERT_MODE_GRAD: return launch_enum_mode<PERT_MODE_GRAD>(prob->P, grid, *prob, s2, *hp, stream);
+    case PERT_MODE_DECODE: return launch_enum_mode<PERT_MODE_DECODE>(prob->P, grid, *prob, s2, *hp, stream);
+    default: return PERT_E_ARG;
+  }
+}
+
+int pert_obs_pass(const pert_problem* prob, pert_state* st, hipStream_t stream) {
+  if (!problem_ok(prob) || !st || prob->kind != PERT_KIND_STEP1) return PERT_E_ARG;
+  if (!prob->cn_obs || !prob->rep_obs || !st->cell_part || !st->bin_part || !st->blk_part) return PERT_E_ARG;
+  pert_state s2 = *st;
+  s2.bins_per_tile = tile_bins(st);
+  const dim3 grid((prob->N + kBlock - 1) / kBlock, (prob->L + s2.bins_per_tile - 1) / s2.bins_per_tile);
+  hipLaunchKernelGGL(obs_kernel, grid, dim3(kBlock), 0, stream, *prob, s2);
+  return hip_status(hipGetLastError());
+}
+
+int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream) {
+  if (!problem_ok(prob) || !st || !st->grad_shared || !st->grad_cell || !st->cellblk_part) return PERT_E_ARG;
+  pert_state s2 = *st;
+  s2.bins_per_tile = tile_bins(st);
+  const int lt = s2.bins_per_tile;
+  const int n_ct = (prob->N + kBlock - 1) / kBlock;
+  const int n_bt = (prob->L + lt - 1) / lt;
+  const int n_lblk = (prob->L + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(finalize_kernel, dim3(n_ct + n_lblk), dim3(kBlock), 0, stream, *prob, s2, n_ct,
+                     n_bt, n_ct);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_status(e);
+  hipLaunchKernelGGL(scalar_kernel, dim3(1), dim3(kBlock), 0, stream, *prob, s2, n_bt * n_ct, n_ct);
+  return hip_status(hipGetLastError());
+}
+
+int pert_adam(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp, hipStream_t stream) {
+  if (!prob || !st || !hp || !st->params || !st->adam_m || !st->adam_v) return PERT_E_ARG;
+  const int n = st->lay.n_params;
+  hipLaunchKernelGGL(adam_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, *prob, *st, *hp);
+  return hip_status(hipGetLastError());
+}
+
+int pert_selftest_nb_lgdiff_host(int64_t n, const float* d, const float* x, float* lam, float* psi) {
+  for (int64_t i = 0; i < n; ++i) {
+    const float xi = x[i];
+    nb_lgdiff(d[i], xi, xi > 0.0f ? 1.0f / xi : 0.0f, lam[i], psi[i]);
+  }
+  return PERT_OK;
+}
+
+int pert_selftest_nb_lgdiff_device(int64_t n, const float* d, const float* x, float* lam, float* psi,
+                                   hipStream_t stream) {
+  if (n <= 0) return PERT_OK;
+  hipLaunchKernelGGL(nb_selftest_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, n, d, x,
+                     lam, psi);
+  return hip_status(hipGetLastError());
+}
+
+int pert_selftest_enum_cellbin_host(int32_t P, int64_t n, const float* x, const float* em1,
+                                    const float* S1, const float* z, float log1m_lam, const float* D,
+                                    const float* phi, float* E, float* dirv, float* gD, float* gt,
+                                    float* gz, int32_t* amax) {
+  switch (P) {
+#define PERT_CASE(PP) \
+  case PP: return selftest_enum_host<PP>(n, x, em1, S1, z, log1m_lam, D, phi, E, dirv, gD, gt, gz, amax);
+    PERT_CASE(2) PERT_CASE(3) PERT_CASE(4) PERT_CASE(5) PERT_CASE(6) PERT_CASE(7) PERT_CASE(8)
+    PERT_CASE(9) PERT_CASE(10) PERT_CASE(11) PERT_CASE(12) PERT_CASE(13) PERT_CASE(14)
+    PERT_CASE(15) PERT_CASE(16)
+#undef PERT_CASE
+    default: return PERT_E_UNSUPPORTED_P;
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,275 @@
+// pert_math.h -- per (bin, cell) arithmetic of the PERT log joint, shared by the
+// gfx950 kernels (pert_kernels.hip) and the host self-test entry points.
+//
+// Everything here restates reference scdna_replication_tools/pert_model.py:607-646
+// plus the torch.distributions log densities Pyro wraps:
+//
+//   s(c, r) = log pi~_c + log Bern(r | phi) + NB'(chi = c (1 + r))
+//   NB'(chi) = delta_chi log(1 - lam) + Lambda(delta_chi, x)
+//   Lambda(d, x) = lgamma(d + x) - lgamma(d) - (x log x - x)
+//
+// The chi-independent remainder of the NB log density, x log(lam) - lgamma(1 + x)
+// + (x log x - x), is parameter independent in steps 2/3 and is added on the host
+// once (kappa(x) in DESIGN.md).  Subtracting x log x - x from lgamma(d + x) keeps
+// every per-state score O(100) instead of O(x log x), so the fp32 differences
+// that decide the responsibilities stay accurate.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PERT_HD __host__ __device__ __forceinline__
+
+namespace pert {
+
+constexpr float kLn2 = 0.693147180559945309f;
+constexpr float kLog2e = 1.442695040888963407f;
+constexpr float kEps32 = 1.1920928955078125e-07f;   // torch.finfo(float32).eps (clamp_probs)
+constexpr float kTiny32 = 1.1754943508222875e-38f;  // torch.finfo(float32).tiny (_clipped_sigmoid)
+constexpr float kHalfLog2Pi = 0.918938533204672742f;
+constexpr float kLogEps32 = -15.942385152878742f;    // log(eps)
+constexpr float kLog1mEps32 = -1.1920929665620896e-07f;  // log(1 - eps)
+
+// ----------------------------------------------------------------- primitives
+// v_log_f32 / v_exp_f32 / v_rcp_f32 on the device; libm on the host self-test.
+PERT_HD float flog(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_logf(x) * kLn2;
+#else
+  return logf(x);
+#endif
+}
+PERT_HD float fexp(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_exp2f(x * kLog2e);
+#else
+  return expf(x);
+#endif
+}
+PERT_HD float frcp(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rcpf(x);
+#else
+  return 1.0f / x;
+#endif
+}
+
+// log1p(q) for q >= 0 given inv_u ~= 1/(1+q): the rounding error of 1+q is added
+// back (q - ((1+q) - 1)) / (1+q) -- exact to a few ulp of the result.
+PERT_HD float log1p_corr(float q, float inv_u) {
+  float u = 1.0f + q;
+  return flog(u) + (q - (u - 1.0f)) * inv_u;
+}
+
+// Stirling remainder S(z) = 1/(12 z) - 1/(360 z^3) + 1/(1260 z^5), z >= 8 (|err| < 4e-10).
+PERT_HD float stirling_rem(float rz) {
+  float rz2 = rz * rz;
+  return rz * (0.0833333333333333333f - rz2 * (0.00277777777777777778f - rz2 * 0.000793650793650793651f));
+}
+
+// Lambda(d, x) = lgamma(d+x) - lgamma(d) - (x log x - x)  and  Psi(d, x) = digamma(d+x) - digamma(d)
+// for d >= 1, x >= 0 (x integer valued as in pert_model.py:163-166; any x >= 0 works).
+// invx = 1/x (0 when x == 0).
+//   d >= 8: asymptotic series on both arguments in cancellation-free form
+//     (d - 1/2) log1p(x/d) + x log1p(d/x) + S(d+x) - S(d)
+//   d <  8: shift d by k = ceil(8 - d) <= 7 with the recurrences
+//     lgamma(y) = lgamma(y + k) - log prod_{i<k} (y + i),  digamma(y) = digamma(y + k) - sum 1/(y + i).
+PERT_HD void nb_lgdiff(float d, float x, float invx, float& lam, float& psi) {
+  float corr_l = 0.0f, corr_p = 0.0f;
+  if (d < 8.0f) {
+    const float kf = ceilf(8.0f - d);
+    float num_a = 1.0f, num_b = 1.0f, den = 1.0f;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const bool on = (float)i < kf;
+      const float di = d + (float)i;
+      const float dxi = di + x;
+      if (i < 4) num_a *= on ? dxi : 1.0f; else num_b *= on ? dxi : 1.0f;
+      den *= on ? di : 1.0f;
+      corr_p += on ? x * frcp(di * dxi) : 0.0f;        // 1/di - 1/dxi
+    }
+    corr_l = -(flog(num_a) + flog(num_b) - flog(den));
+    d += kf;
+  }
+  const float r = frcp(d);
+  const float zs = d + x;
+  const float rz = frcp(zs);
+  const float l1 = log1p_corr(x * r, d * rz);         // log1p(x/d)
+  const float l2 = log1p_corr(d * invx, x * rz);      // log1p(d/x); 0 when x == 0
+  lam = (d - 0.5f) * l1 + x * l2 + (stirling_rem(rz) - stirling_rem(r)) + corr_l;
+  const float r2 = r * r, rz2 = rz * rz;
+  const float r4 = r2 * r2, rz4 = rz2 * rz2;
+  psi = l1 - 0.5f * (rz - r) - 0.0833333333333333333f * (rz2 - r2)
+        + 0.00833333333333333333f * (rz4 - r4) - 0.00396825396825396825f * (rz4 * rz2 - r4 * r2)
+        + corr_p;
+}
+
+// Number of CN states P is a compile-time constant of every kernel; chi = c (1 + r)
+// takes the values 0..P-1 (r = 0) and the even values 0..2P-2 (r = 1).
+template <int P>
+PERT_HD constexpr bool chi_needed(int chi) { return chi < P || (chi % 2) == 0; }
+
+// ----------------------------------------------------------------- enumerated cell.bin
+// One (bin, cell) of the step-2/3 enumerated log joint: forward, responsibilities
+// and the analytic backward.
+template <int P>
+struct EnumOut {
+  float E;        // logsumexp_{c,r} s(c, r)                        (pert_model.py:607-646, B.1)
+  float dirv;     // sum_k (eta_k - 1) log pi_k                     (dirichlet.py:93-97, variable part)
+  float gD;       // dE/dD, D = u omega (1-lam)/lam                 (delta = chi D, mask delta >= 1)
+  float gt;       // dE/dt / a, t = tau - rho                        (masked where phi clamped)
+  float gz[P];    // d(E + dirv)/dz_k (z = unconstrained pi logits)
+  int   argmax;   // r * P + c of the joint MAP state               (infer_discrete, B.7)
+};
+
+template <int P, bool WANT_GRAD, bool WANT_ARGMAX>
+PERT_HD void enum_cellbin(float x, float invx, const float (&em1)[P], float S1, const float (&z)[P],
+                          float log1m_lam, float D, float phi_raw, EnumOut<P>& o) {
+  // Bernoulli(phi) with the in-place clamps of pert_model.py:622-623
+  float phic = phi_raw;
+  bool mphi = true;
+  if (phic < 0.001f) { phic = 0.001f; mphi = false; }
+  if (phic > 0.999f) { phic = 0.999f; mphi = false; }
+  const float lphi = flog(phic);
+  const float l1mphi = flog(1.0f - phic);
+
+  // pi = softmax(z) (SoftmaxTransform, transforms.py:951-954) and the Categorical log
+  // pmf log(clamp_probs(pi)) (categorical.py:67-71, utils.py clamp_probs)
+  float m = z[0];
+  int jmax = 0;
+#pragma unroll
+  for (int k = 1; k < P; ++k) { if (z[k] > m) { m = z[k]; jmax = k; } }
+  float e[P];
+  float t = 0.0f;
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    e[k] = (k == jmax) ? 1.0f : fexp(z[k] - m);
+    t += (k == jmax) ? 0.0f : e[k];
+  }
+  const float inv1t = frcp(1.0f + t);
+  const float lse1p = log1p_corr(t, inv1t);
+  float pi[P], lc[P];
+  bool mk[P];
+  float dirv = 0.0f;
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const float logpi = (z[k] - m) - lse1p;
+    pi[k] = e[k] * inv1t;
+    const float om = (k == jmax) ? t * inv1t : 1.0f - pi[k];
+    const bool hi = om < kEps32;
+    const bool lo = pi[k] < kEps32;
+    mk[k] = !(hi || lo);
+    lc[k] = hi ? kLog1mEps32 : (lo ? kLogEps32 : logpi);
+    dirv += em1[k] * logpi;
+  }
+  o.dirv = dirv;
+
+  // negative-binomial part per distinct chi
+  float lam1, psi1;
+  nb_lgdiff(1.0f, x, invx, lam1, psi1);
+  const float n_clamped = log1m_lam + lam1;   // delta == 1 (chi == 0 or chi D < 1)
+  float Nc[2 * P - 1], Bc[2 * P - 1];
+  Nc[0] = n_clamped;
+  Bc[0] = 0.0f;
+#pragma unroll
+  for (int chi = 1; chi < 2 * P - 1; ++chi) {
+    if (!chi_needed<P>(chi)) continue;
+    const float d = (float)chi * D;
+    if (d < 1.0f) {
+      Nc[chi] = n_clamped;
+      Bc[chi] = 0.0f;
+    } else {
+      float lam, psi;
+      nb_lgdiff(d, x, invx, lam, psi);
+      Nc[chi] = d * log1m_lam + lam;
+      Bc[chi] = (float)chi * (log1m_lam + psi);
+    }
+  }
+
+  // joint scores, logsumexp over the 2P states (r-major like the oracle's (2, P) layout)
+  float s[2 * P];
+  float smax = -INFINITY;
+  int amax = 0;
+#pragma unroll
+  for (int c = 0; c < P; ++c) {
+    s[c] = lc[c] + l1mphi + Nc[c];
+    s[P + c] = lc[c] + lphi + Nc[2 * c];
+  }
+#pragma unroll
+  for (int i = 0; i < 2 * P; ++i) { if (s[i] > smax) { smax = s[i]; amax = i; } }
+  if (WANT_ARGMAX) o.argmax = amax;
+  if (!WANT_GRAD) { o.E = smax; return; }
+  float se = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 2 * P; ++i) { s[i] = fexp(s[i] - smax); se += s[i]; }
+  const float inv_se = frcp(se);
+  o.E = smax + flog(se);
+
+  float gD = 0.0f, g1 = 0.0f, sgm = 0.0f;
+  float gcn[P];
+#pragma unroll
+  for (int c = 0; c < P; ++c) {
+    const float g0c = s[c] * inv_se, g1c = s[P + c] * inv_se;
+    gD += g0c * Bc[c] + g1c * Bc[2 * c];
+    g1 += g1c;
+    gcn[c] = g0c + g1c;
+    sgm += mk[c] ? gcn[c] : 0.0f;
+  }
+  o.gD = gD;
+  o.gt = mphi ? (g1 - phic) : 0.0f;
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    // (eta_k - 1) - pi_k S1 in the cancellation-free form (Appendix C) + Categorical term
+    o.gz[k] = em1[k] - pi[k] * S1 + (mk[k] ? gcn[k] : 0.0f) - pi[k] * sgm;
+  }
+}
+
+// ----------------------------------------------------------------- observed cell.bin (step 1)
+// NB + Bernoulli terms with cn / rep observed (pert_model.py:724-729, JitTrace_ELBO).
+struct ObsOut {
+  float ll;      // delta log(1-lam) + Lambda(delta, x) + log Bern(rep | phi)
+  float gD;      // d ll / dD            (chi (log(1-lam) + Psi) masked on delta >= 1)
+  float dsum;    // delta (clamped value) -- d/dlam of delta log(1-lam) is -delta/(1-lam)
+  float gdd;     // (log(1-lam) + Psi) delta, masked -- enters d/dlam through ddelta/dlam
+  float gt;      // d ll / dt / a
+};
+
+PERT_HD void obs_cellbin(float x, float invx, float cn, float rep, float log1m_lam, float D,
+                         float phi_raw, ObsOut& o) {
+  float phic = phi_raw;
+  bool mphi = true;
+  if (phic < 0.001f) { phic = 0.001f; mphi = false; }
+  if (phic > 0.999f) { phic = 0.999f; mphi = false; }
+  o.ll = rep > 0.5f ? flog(phic) : flog(1.0f - phic);
+  o.gt = mphi ? (rep - phic) : 0.0f;
+  const float chi = cn * (1.0f + rep);
+  float d = chi * D;
+  float lam, psi;
+  if (d < 1.0f) {
+    nb_lgdiff(1.0f, x, invx, lam, psi);
+    o.ll += log1m_lam + lam;
+    o.gD = 0.0f;
+    o.gdd = 0.0f;
+    o.dsum = 1.0f;
+  } else {
+    nb_lgdiff(d, x, invx, lam, psi);
+    o.ll += d * log1m_lam + lam;
+    const float g = log1m_lam + psi;
+    o.gD = chi * g;
+    o.gdd = d * g;
+    o.dsum = d;
+  }
+}
+
+// ----------------------------------------------------------------- transforms
+// _clipped_sigmoid (torch/distributions/transforms.py:629-631); *mask = 0 where clipped.
+PERT_HD float clipped_sigmoid(float zz, float* dmask) {
+  float s = frcp(1.0f + fexp(-zz));
+  float ds = s * (1.0f - s);
+  if (s < kTiny32) { s = kTiny32; ds = 0.0f; }
+  if (s > 1.0f - kEps32) { s = 1.0f - kEps32; ds = 0.0f; }
+  *dmask = ds;
+  return s;
+}
+
+}  // namespace pert

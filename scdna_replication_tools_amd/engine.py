@@ -1,0 +1,465 @@
+"""Device-resident SVI state for one cell shard and the per-step launch sequence.
+
+A ``PertShard`` owns every buffer of one fit (step 1, 2 or 3 of reference
+``pert_model.run_pert_model``, pert_model.py:649-901) on one GPU:
+
+* inputs: reads (L, N) fp32, gc features (L, K+1), library index (N,), the CN
+  prior eta as a code book (uint16 codes (L, N) + table) for steps 2/3, the
+  observed cn / rep (uint8) for step 1;
+* the pi logits and their Adam moments as (L, P, N) planes (steps 2/3);
+* the packed non-pi parameters (layout ``pert_layout`` of include/pert_hip.h),
+  their Adam moments and gradients.
+
+``step()`` is one ``svi.step`` (pert_model.py:743 / :801 / :868): enumerated or
+observed pass with the fused pi Adam update, reductions, the cross-rank
+all-reduce of the shared-gradient block (rho, a, beta_stds, lambda, beta_means,
+loss) when a process group is given, and Adam on the packed parameters.
+Everything runs through libpert_hip.so; there is no host fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+from typing import Callable, Dict, Optional
+
+import numpy as np
+import torch
+
+from . import _native as nat
+
+ADAM_BETAS = (0.8, 0.99)
+ADAM_EPS = 1e-8
+F32 = np.float32
+EPS32 = float(np.finfo(np.float32).eps)
+TINY32 = float(np.finfo(np.float32).tiny)
+
+
+# --------------------------------------------------------------------------- transforms
+# torch.distributions.transform_to semantics (constraint_registry.py), fp32.
+def sigmoid_inv(y: torch.Tensor) -> torch.Tensor:
+    y = y.clamp(min=TINY32, max=1.0 - EPS32)
+    return y.log() - (-y).log1p()
+
+
+def clipped_sigmoid(z: torch.Tensor) -> torch.Tensor:
+    return torch.clamp(torch.sigmoid(z), min=TINY32, max=1.0 - EPS32)
+
+
+def gc_features(gc: np.ndarray, K: int) -> torch.Tensor:
+    """pert_model.py:460-463 evaluated like the reference (fp32 torch): [gc^K .. gc, 1]."""
+    x = torch.as_tensor(np.asarray(gc), dtype=torch.float32).unsqueeze(1)
+    return torch.cat([x ** i for i in reversed(range(0, K + 1))], 1)
+
+
+# --------------------------------------------------------------------------- CN prior code book
+@dataclass
+class EtaCodebook:
+    """The (L, N, P) Dirichlet concentration eta stored as uint16 row codes + table.
+
+    Every eta builder of the reference (pert_model.py:272-361, :668-716) yields rows
+    drawn from a small set (one weight on one state, or the composite sums), so the
+    (L, N, P) fp32 tensor (2.8 GB at 10k cells x 5.5k bins) shrinks to 2 B per cell.bin.
+    """
+    codes: np.ndarray   # (L, N) uint16
+    table: np.ndarray   # (n_codes, P) float32 eta rows
+
+    @property
+    def P(self):
+        return self.table.shape[1]
+
+    @classmethod
+    def from_dense(cls, etas) -> "EtaCodebook":
+        e = np.ascontiguousarray(np.asarray(etas, dtype=F32))
+        L, N, P = e.shape
+        table, inv = np.unique(e.reshape(-1, P), axis=0, return_inverse=True)
+        if table.shape[0] > 65535:
+            raise ValueError("eta has {} distinct rows; at most 65535 are supported".format(table.shape[0]))
+        return cls(inv.reshape(L, N).astype(np.uint16), table.astype(F32))
+
+    @classmethod
+    def from_states(cls, states, weight: float, P: int) -> "EtaCodebook":
+        """build_cn_prior (pert_model.py:272-282): ones with eta[state] = weight."""
+        s = np.asarray(states).astype(np.int64)
+        if s.min() < 0 or s.max() >= P:
+            raise ValueError("CN states must lie in [0, P) for P={}".format(P))
+        table = np.ones((P, P), dtype=F32)
+        table[np.arange(P), np.arange(P)] = F32(weight)
+        return cls(s.astype(np.uint16), table)
+
+    def kernel_table(self) -> np.ndarray:
+        """(n_codes, P+1): eta_k - 1, then S1 = sum_k (eta_k - 1) (include/pert_hip.h)."""
+        em1 = self.table.astype(np.float64) - 1.0
+        out = np.concatenate([em1, em1.sum(1, keepdims=True)], axis=1)
+        return out.astype(F32)
+
+    def counts(self) -> np.ndarray:
+        return np.bincount(self.codes.reshape(-1), minlength=self.table.shape[0])
+
+    def dirichlet_normaliser(self, mode: str = "torch32") -> float:
+        """sum_{l,n} lgamma(sum eta) - sum lgamma(eta).  ``torch32`` evaluates each row in
+        fp32 exactly as torch.distributions.Dirichlet.log_prob does on the CPU
+        (dirichlet.py:93-97) -- the constant the reference adds to every loss --
+        ``exact`` in fp64."""
+        t = torch.from_numpy(self.table)
+        if mode == "exact":
+            t = t.double()
+        per = (torch.lgamma(t.sum(-1)) - torch.lgamma(t).sum(-1)).double().numpy()
+        return float((per * self.counts()).sum())
+
+    def argmax_states(self) -> np.ndarray:
+        """torch.argmax(etas, dim=2) (first max), pert_model.py:591-592 and :439."""
+        row_arg = np.argmax(self.table, axis=1)
+        return row_arg[self.codes]
+
+    def dense(self) -> np.ndarray:
+        return self.table[self.codes]
+
+
+def kappa_sum(reads: np.ndarray, log_lam: Optional[float]) -> float:
+    """sum over (bin, cell) of the parameter-free part of the NB log density that the
+    kernels leave out: (x log lam) + (x log x - x) - lgamma(1 + x)."""
+    x = torch.as_tensor(np.asarray(reads), dtype=torch.float64)
+    xlx = torch.where(x > 0, x * torch.log(torch.where(x > 0, x, torch.ones_like(x))), torch.zeros_like(x))
+    s = float((xlx - x - torch.lgamma(1.0 + x)).sum())
+    if log_lam is not None:
+        s += float(x.sum()) * log_lam
+    return s
+
+
+# --------------------------------------------------------------------------- step-1 pi block
+class CanonicalPiBlock:
+    """Step 1's expose_pi site (pert_model.py:607-613 with etas = ones, cn observed).
+
+    pi(l, n) only enters log Categorical(cn_obs | pi) and the constant Dirichlet(1)
+    density, starts at the uniform simplex for every (l, n), and Adam is
+    element-wise, so every (l, n) follows the same trajectory up to a permutation
+    of the states.  One P-vector reproduces all of them exactly; its loss term is
+    L * N * log pi~_c(t).
+    """
+
+    def __init__(self, P: int, lr: float, betas=ADAM_BETAS, eps=ADAM_EPS):
+        self.P = P
+        self.z = np.full(P, np.log(F32(1.0 / P)), dtype=F32)
+        self.m = np.zeros(P, F32)
+        self.v = np.zeros(P, F32)
+        self.lr, self.b1, self.b2, self.eps = lr, betas[0], betas[1], eps
+
+    def logp_and_grad(self):
+        z = torch.from_numpy(self.z.copy()).requires_grad_(True)
+        p = torch.softmax(z, 0)
+        p = p / p.sum()
+        lp = torch.log(torch.clamp(p, min=EPS32, max=1 - EPS32))[0]   # observed state at index 0
+        lp.backward()
+        return float(lp), (-z.grad).numpy().astype(F32)             # loss gradient
+
+    def step(self, t: int) -> float:
+        lp, g = self.logp_and_grad()
+        self.m = (self.b1 * self.m + (1 - self.b1) * g).astype(F32)
+        self.v = (self.b2 * self.v + (1 - self.b2) * g * g).astype(F32)
+        bc1 = 1 - self.b1 ** t
+        bc2 = 1 - self.b2 ** t
+        denom = np.sqrt(self.v) / math.sqrt(bc2) + self.eps
+        self.z = (self.z - (self.lr / bc1) * self.m / denom).astype(F32)
+        return lp
+
+
+# --------------------------------------------------------------------------- shard
+def _ptr(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else int(t.data_ptr())
+
+
+class PertShard:
+    """One fit (kind 1/2/3) over one contiguous cell shard, resident on one GPU."""
+
+    def __init__(self, kind: int, reads, gc, libs, n_libs: int, P: int, K: int, init: Dict[str, np.ndarray],
+                 *, eta: Optional[EtaCodebook] = None, cn_obs=None, rep_obs=None,
+                 lamb: Optional[float] = None, beta_means=None, rho_fixed=None, a_fixed: Optional[float] = None,
+                 pi_init=None, device=None, lr: float = 0.05, betas=ADAM_BETAS, eps: float = ADAM_EPS,
+                 is_root: bool = True, n_cells_total: Optional[int] = None,
+                 allreduce: Optional[Callable[[torch.Tensor], None]] = None,
+                 dirichlet_mode: str = "torch32", bins_per_tile: int = 0):
+        self.lib = nat.lib()
+        self.kind = int(kind)
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise ValueError("PertShard needs a GPU device (got {})".format(self.device))
+        reads = np.asarray(reads)
+        L, N = reads.shape
+        self.L, self.N, self.P, self.K, self.K1, self.n_libs = L, N, int(P), int(K), int(K) + 1, int(n_libs)
+        if not (nat.MIN_P <= self.P <= nat.MAX_P):
+            raise ValueError("P={} unsupported (2..16)".format(P))
+        if self.K1 > nat.MAX_K1:
+            raise ValueError("K={} unsupported (K+1 <= 8)".format(K))
+        self.n_cells_total = N if n_cells_total is None else int(n_cells_total)
+        self.lr, self.betas, self.eps = float(lr), tuple(betas), float(eps)
+        self.allreduce = allreduce
+        self.t = 0
+        dev = self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+
+        # ---- inputs (pert_model.py:133-191 layouts)
+        self.reads = torch.as_tensor(reads.astype(F32), device=dev).contiguous()
+        self.gcf = gc_features(gc, self.K).to(dev).contiguous()
+        self.libs = torch.as_tensor(np.asarray(libs).astype(np.int32), device=dev)
+        x64 = reads.astype(np.float64)
+        mean_reads = torch.mean(torch.as_tensor(reads, dtype=torch.float32), dim=0)
+        self.mean_reads = mean_reads.to(dev)
+        if self.kind == nat.KIND_STEP1:
+            ploidy = np.full(N, 2.0, dtype=F32)                                       # :595
+        else:
+            if eta is None:
+                raise ValueError("steps 2/3 need the CN prior eta")
+            if eta.P != self.P or eta.codes.shape != (L, N):
+                raise ValueError("eta code book does not match (L, N, P)")
+            ploidy = torch.mean(torch.as_tensor(eta.argmax_states(), dtype=torch.float32), dim=0).numpy()  # :591-593
+        self.ploidy = torch.as_tensor(ploidy, dtype=torch.float32, device=dev)
+
+        self.eta = eta
+        self.eta_code = self.eta_table = None
+        self.cn_obs = self.rep_obs = None
+        self.beta_means_t = self.rho_fixed_t = None
+        lam_f = 0.0
+        if self.kind == nat.KIND_STEP1:
+            cn = np.asarray(cn_obs)
+            if cn.min() < 0 or cn.max() >= self.P:
+                raise ValueError("observed CN states must lie in [0, P)")
+            self.cn_obs = torch.as_tensor(cn.astype(np.uint8), device=dev).contiguous()
+            self.rep_obs = torch.as_tensor(np.asarray(rep_obs).astype(np.uint8), device=dev).contiguous()
+        else:
+            self.eta_code = torch.as_tensor(np.ascontiguousarray(eta.codes, dtype=np.uint16).view(np.int16), device=dev)
+            self.eta_table = torch.as_tensor(eta.kernel_table(), device=dev).contiguous()
+            lam_f = float(np.asarray(lamb, dtype=F32).reshape(-1)[0])
+            self.beta_means_t = torch.as_tensor(np.asarray(beta_means, dtype=F32).reshape(self.n_libs, self.K1),
+                                                device=dev).contiguous()
+            if self.kind == nat.KIND_STEP3:
+                self.rho_fixed_t = torch.as_tensor(np.asarray(rho_fixed, dtype=F32).reshape(L), device=dev)
+        self.lamb = lam_f
+
+        # ---- packed parameters (include/pert_hip.h pert_layout)
+        self.lay = nat.make_layout(L, N, self.K1, self.n_libs)
+        lay = self.lay
+        self.params = torch.zeros(lay.n_params, **f32)
+        self.adam_m = torch.zeros(lay.n_params, **f32)
+        self.adam_v = torch.zeros(lay.n_params, **f32)
+        self.grad_shared = torch.zeros(lay.n_shared + 1, dtype=torch.float64, device=dev)
+        self.grad_cell = torch.zeros(lay.n_params - lay.n_shared, **f32)
+        self._load_init(init)
+
+        self.z_pi = self.m_pi = self.v_pi = None
+        self.g_pi = None
+        if self.kind != nat.KIND_STEP1:
+            if pi_init is None:
+                # AutoDelta init of the multivariate Dirichlet site: transform_to(simplex)(0) -> 1/P
+                z0 = float(torch.log(torch.tensor(1.0 / self.P, dtype=torch.float32)))
+                self.z_pi = torch.full((L, self.P, N), z0, **f32)
+            else:
+                pi0 = torch.as_tensor(np.asarray(pi_init), dtype=torch.float32)
+                self.z_pi = pi0.log().permute(0, 2, 1).contiguous().to(dev)              # SoftmaxTransform.inv
+            self.m_pi = torch.zeros_like(self.z_pi)
+            self.v_pi = torch.zeros_like(self.z_pi)
+        self.cn_out = torch.zeros((L, N), dtype=torch.uint8, device=dev)
+        self.rep_out = torch.zeros((L, N), dtype=torch.uint8, device=dev)
+
+        ncp, nbp, nblk, ncb = nat.workspace_sizes(self.kind, L, N, self.K1, self.n_libs, bins_per_tile)
+        self.cell_part = torch.zeros(ncp, **f32)
+        self.bin_part = torch.zeros(nbp, **f32)
+        self.blk_part = torch.zeros(nblk, dtype=torch.float64, device=dev)
+        self.cellblk_part = torch.zeros(ncb, dtype=torch.float64, device=dev)
+        self.bins_per_tile = int(bins_per_tile)
+        self.pass_events = None      # list -> (start, end) HIP events around every pass
+
+        # ---- constants of the loss (added on the host, summed over ranks once)
+        if self.kind == nat.KIND_STEP1:
+            const = kappa_sum(x64, None) + L * N * math.lgamma(self.P)   # Dirichlet(ones) normaliser
+            self.sum_reads = float(x64.sum())
+            self.pi_block = CanonicalPiBlock(self.P, self.lr, self.betas, self.eps)
+        else:
+            const = kappa_sum(x64, math.log(lam_f)) + eta.dirichlet_normaliser(dirichlet_mode)
+            self.sum_reads = 0.0
+            self.pi_block = None
+        c = torch.tensor([const], dtype=torch.float64, device=dev)
+        if self.allreduce is not None:
+            self.allreduce(c)
+        self.const_total = float(c.item())
+
+        # ---- C structs
+        self._prob = nat.PertProblem(
+            kind=self.kind, L=L, N=N, P=self.P, K1=self.K1, n_libs=self.n_libs,
+            n_codes=0 if eta is None else int(eta.table.shape[0]), is_root=1 if is_root else 0,
+            reads=_ptr(self.reads), gcf=_ptr(self.gcf), libs=_ptr(self.libs), eta_code=_ptr(self.eta_code),
+            eta_table=_ptr(self.eta_table), cn_obs=_ptr(self.cn_obs), rep_obs=_ptr(self.rep_obs),
+            mean_reads=_ptr(self.mean_reads), ploidy=_ptr(self.ploidy), lamb=lam_f,
+            log1m_lam=(math.log1p(-lam_f) if self.kind != nat.KIND_STEP1 else 0.0),
+            sum_reads=self.sum_reads, a_fixed=float(a_fixed) if a_fixed is not None else 0.0,
+            beta_means=_ptr(self.beta_means_t), rho_fixed=_ptr(self.rho_fixed_t))
+        self._state = nat.PertState(
+            lay=lay, params=_ptr(self.params), adam_m=_ptr(self.adam_m), adam_v=_ptr(self.adam_v),
+            grad_shared=_ptr(self.grad_shared), grad_cell=_ptr(self.grad_cell), z_pi=_ptr(self.z_pi),
+            m_pi=_ptr(self.m_pi), v_pi=_ptr(self.v_pi), g_pi=0, cn_out=_ptr(self.cn_out),
+            rep_out=_ptr(self.rep_out), cell_part=_ptr(self.cell_part), bin_part=_ptr(self.bin_part),
+            blk_part=_ptr(self.blk_part), cellblk_part=_ptr(self.cellblk_part),
+            bins_per_tile=self.bins_per_tile)
+        self._hp = nat.PertAdamHparams(lr=self.lr, beta1=self.betas[0], beta2=self.betas[1], eps=self.eps,
+                                       step_size=0.0, inv_bc2_sqrt=0.0)
+
+    # ------------------------------------------------------------------ params
+    def _load_init(self, init: Dict[str, np.ndarray]):
+        lay, L, N, K1, nl = self.lay, self.L, self.N, self.K1, self.n_libs
+        p = torch.zeros(lay.n_params, dtype=torch.float32)
+
+        def t32(v):
+            return torch.as_tensor(np.asarray(v, dtype=np.float64), dtype=torch.float32)
+        if self.kind != nat.KIND_STEP3:
+            p[lay.off_rho:lay.off_rho + L] = sigmoid_inv(t32(init["expose_rho"]).reshape(L))
+            p[lay.off_a] = torch.log(t32(init["expose_a"]).reshape(-1)[0])
+        if self.kind == nat.KIND_STEP1:
+            lam = t32(init["expose_lambda"]).reshape(-1)[0]
+            p[lay.off_lam] = sigmoid_inv((lam - 0.001) / 0.998)
+            p[lay.off_bmeans:lay.off_bmeans + nl * K1] = t32(init["expose_beta_means"]).reshape(-1)
+        p[lay.off_bstds:lay.off_bstds + nl * K1] = torch.log(t32(init["expose_beta_stds"]).reshape(-1))
+        p[lay.off_u:lay.off_u + N] = t32(init["expose_u"]).reshape(N)
+        p[lay.off_beta:lay.off_beta + K1 * N] = t32(init["expose_betas"]).reshape(N, K1).t().reshape(-1)
+        p[lay.off_tau:lay.off_tau + N] = sigmoid_inv(t32(init["expose_tau"]).reshape(N))
+        self.params.copy_(p.to(self.device))
+
+    def set_unconstrained(self, z: Dict[str, np.ndarray]):
+        """Overwrite the state with explicit unconstrained values (oracle site names)."""
+        lay, L, N, K1, nl = self.lay, self.L, self.N, self.K1, self.n_libs
+        p = self.params.cpu()
+
+        def t32(v):
+            return torch.as_tensor(np.asarray(v, dtype=np.float64), dtype=torch.float32)
+        if "expose_rho" in z:
+            p[lay.off_rho:lay.off_rho + L] = t32(z["expose_rho"]).reshape(L)
+        if "expose_a" in z:
+            p[lay.off_a] = t32(z["expose_a"]).reshape(-1)[0]
+        if "expose_lambda" in z:
+            p[lay.off_lam] = t32(z["expose_lambda"]).reshape(-1)[0]
+        if "expose_beta_means" in z and self.kind == nat.KIND_STEP1:
+            p[lay.off_bmeans:lay.off_bmeans + nl * K1] = t32(z["expose_beta_means"]).reshape(-1)
+        p[lay.off_bstds:lay.off_bstds + nl * K1] = t32(z["expose_beta_stds"]).reshape(-1)
+        p[lay.off_u:lay.off_u + N] = t32(z["expose_u"]).reshape(N)
+        p[lay.off_beta:lay.off_beta + K1 * N] = t32(z["expose_betas"]).reshape(N, K1).t().reshape(-1)
+        p[lay.off_tau:lay.off_tau + N] = t32(z["expose_tau"]).reshape(N)
+        self.params.copy_(p.to(self.device))
+        if "expose_pi" in z and self.z_pi is not None:
+            self.z_pi.copy_(t32(z["expose_pi"]).permute(0, 2, 1).contiguous().to(self.device))
+
+    def constrained(self) -> Dict[str, np.ndarray]:
+        """Current constrained site values (what the reference's trace exposes)."""
+        lay, L, N, K1, nl = self.lay, self.L, self.N, self.K1, self.n_libs
+        p = self.params.cpu()
+        out = {}
+        if self.kind != nat.KIND_STEP3:
+            out["expose_rho"] = clipped_sigmoid(p[lay.off_rho:lay.off_rho + L]).numpy().reshape(L, 1)
+            out["expose_a"] = torch.exp(p[lay.off_a:lay.off_a + 1]).numpy()
+        if self.kind == nat.KIND_STEP1:
+            out["expose_lambda"] = (0.001 + 0.998 * clipped_sigmoid(p[lay.off_lam:lay.off_lam + 1])).numpy()
+            out["expose_beta_means"] = p[lay.off_bmeans:lay.off_bmeans + nl * K1].numpy().reshape(nl, K1)
+        out["expose_beta_stds"] = torch.exp(p[lay.off_bstds:lay.off_bstds + nl * K1]).numpy().reshape(nl, K1)
+        out["expose_u"] = p[lay.off_u:lay.off_u + N].numpy().copy()
+        out["expose_betas"] = p[lay.off_beta:lay.off_beta + K1 * N].numpy().reshape(K1, N).T.copy()
+        out["expose_tau"] = clipped_sigmoid(p[lay.off_tau:lay.off_tau + N]).numpy()
+        return out
+
+    def pi(self) -> torch.Tensor:
+        """Constrained pi (L, N, P) on the device (SoftmaxTransform of the logits)."""
+        return torch.softmax(self.z_pi, dim=1).permute(0, 2, 1)
+
+    # ------------------------------------------------------------------ launches
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _set_hparams(self, t: int):
+        b1, b2 = self.betas
+        self._hp.step_size = self.lr / (1.0 - b1 ** t)
+        self._hp.inv_bc2_sqrt = 1.0 / math.sqrt(1.0 - b2 ** t)
+
+    def _pass(self, mode: int):
+        s = self._stream()
+        with torch.cuda.device(self.device):
+            if self.kind == nat.KIND_STEP1:
+                nat.check(self.lib.pert_obs_pass(ctypes.byref(self._prob), ctypes.byref(self._state), s),
+                          "pert_obs_pass")
+            else:
+                nat.check(self.lib.pert_enum_pass(ctypes.byref(self._prob), ctypes.byref(self._state),
+                                                  ctypes.byref(self._hp), mode, s), "pert_enum_pass")
+
+    def _finalize(self):
+        with torch.cuda.device(self.device):
+            nat.check(self.lib.pert_finalize(ctypes.byref(self._prob), ctypes.byref(self._state), self._stream()),
+                      "pert_finalize")
+        if self.allreduce is not None:
+            self.allreduce(self.grad_shared)
+
+    def step_async(self):
+        """One SVI step without reading the loss back (the loss stays on the device)."""
+        self.t += 1
+        self._set_hparams(self.t)
+        if self.pass_events is not None:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            self._pass(nat.MODE_STEP)
+            ev1.record()
+            self.pass_events.append((ev0, ev1))
+        else:
+            self._pass(nat.MODE_STEP)
+        self._finalize()
+        with torch.cuda.device(self.device):
+            nat.check(self.lib.pert_adam(ctypes.byref(self._prob), ctypes.byref(self._state),
+                                         ctypes.byref(self._hp), self._stream()), "pert_adam")
+        if self.pi_block is not None:
+            self._pi_lp = self.pi_block.step(self.t)
+
+    def device_loss(self) -> float:
+        """Loss of the last step: -(ELBO) with the host constants (pert_model.py:743 return value)."""
+        loss = float(self.grad_shared[self.lay.n_shared].item()) - self.const_total
+        if self.pi_block is not None:
+            loss -= self.L * self.n_cells_total * self._pi_lp
+        return loss
+
+    def step(self) -> float:
+        self.step_async()
+        return self.device_loss()
+
+    def loss_and_grads(self):
+        """-ELBO and d(-ELBO)/dz at the current point, without updating (parity tests)."""
+        if self.kind != nat.KIND_STEP1:
+            if self.g_pi is None:
+                self.g_pi = torch.zeros_like(self.z_pi)
+                self._state.g_pi = _ptr(self.g_pi)
+            self._pass(nat.MODE_GRAD)
+        else:
+            self._pass(nat.MODE_GRAD)
+        self._finalize()
+        lay, L, N, K1, nl = self.lay, self.L, self.N, self.K1, self.n_libs
+        gs = self.grad_shared.cpu().numpy()
+        gc = self.grad_cell.cpu().numpy()
+        off = lay.n_shared
+        g = {}
+        if self.kind != nat.KIND_STEP3:
+            g["expose_rho"] = gs[lay.off_rho:lay.off_rho + L].reshape(L, 1)
+            g["expose_a"] = gs[lay.off_a:lay.off_a + 1]
+        if self.kind == nat.KIND_STEP1:
+            g["expose_lambda"] = gs[lay.off_lam:lay.off_lam + 1]
+            g["expose_beta_means"] = gs[lay.off_bmeans:lay.off_bmeans + nl * K1].reshape(nl, K1)
+        g["expose_beta_stds"] = gs[lay.off_bstds:lay.off_bstds + nl * K1].reshape(nl, K1)
+        g["expose_u"] = gc[lay.off_u - off:lay.off_u - off + N]
+        g["expose_betas"] = gc[lay.off_beta - off:lay.off_beta - off + K1 * N].reshape(K1, N).T
+        g["expose_tau"] = gc[lay.off_tau - off:lay.off_tau - off + N]
+        if self.kind != nat.KIND_STEP1:
+            g["expose_pi"] = self.g_pi.permute(0, 2, 1).cpu().numpy()
+        loss = float(gs[lay.n_shared]) - self.const_total
+        if self.pi_block is not None:
+            lp, gpi = self.pi_block.logp_and_grad()
+            loss -= L * self.n_cells_total * lp
+        return loss, g
+
+    def decode(self):
+        """MAP (cn, rep) per (bin, cell): infer_discrete(temperature=0) (pert_model.py:820-827)."""
+        if self.kind == nat.KIND_STEP1:
+            raise ValueError("step 1 has no latent discrete sites")
+        self._pass(nat.MODE_DECODE)
+        return self.cn_out, self.rep_out

@@ -1,0 +1,61 @@
+"""AutoDelta initial values for the three PERT fits (pert_model.py:732, :792, :859).
+
+Pyro's AutoDelta runs the model once under ``init_to_median(num_samples=15)``
+(SURVEY.md Appendix B.4): each univariate latent takes the median of 15 draws from
+its prior, evaluated in model order with earlier sites at their initial values;
+the multivariate Dirichlet site (expose_pi) falls back to a feasible point, which
+``transform_to(simplex)`` maps to the uniform simplex; ``pyro.param`` sites start
+at their declared init (lambda 0.1 :557, beta_stds logspace(0, -K) :561, tau =
+t_init :583).  The draws here come from a ``numpy`` generator seeded with ``seed``
+(same distribution as Pyro's init, not the same random stream);
+``method="median"`` uses the analytic medians instead (the num_samples -> inf
+limit, fully deterministic).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import numpy as np
+from scipy import special, stats
+
+
+def _median15(rng: np.random.Generator, ppf, shape):
+    u = rng.uniform(1e-12, 1 - 1e-12, size=(15,) + tuple(shape))
+    return np.median(ppf(u), axis=0)
+
+
+def init_params(kind: int, reads: np.ndarray, libs: np.ndarray, n_libs: int, P: int, K: int, *,
+                ploidy: Optional[np.ndarray] = None, t_init: Optional[np.ndarray] = None,
+                beta_means: Optional[np.ndarray] = None, seed: int = 0, method: str = "sampled"
+                ) -> Dict[str, np.ndarray]:
+    """Constrained initial site values (float64) keyed by the reference's site names."""
+    L, N = reads.shape
+    K1 = K + 1
+    rng = np.random.default_rng(seed)
+    sampled = method == "sampled"
+    out: Dict[str, np.ndarray] = {}
+    if kind != 3:
+        a_med = special.gammaincinv(2.0, 0.5) / 0.2
+        out["expose_a"] = (np.array([_median15(rng, lambda u: stats.gamma.ppf(u, 2.0, scale=5.0), (1,))[0]])
+                           if sampled else np.array([a_med]))
+    if kind == 1:
+        out["expose_lambda"] = np.array([0.1])
+        out["expose_beta_means"] = (_median15(rng, stats.norm.ppf, (n_libs, K1)) if sampled
+                                    else np.zeros((n_libs, K1)))
+    out["expose_beta_stds"] = np.tile(np.logspace(0, -K, K1)[None, :], (n_libs, 1))
+    if kind != 3:
+        out["expose_rho"] = (_median15(rng, lambda u: u, (L,)) if sampled else np.full(L, 0.5))
+    if kind == 1:
+        tau = (_median15(rng, lambda u: stats.beta.ppf(u, 1.5, 1.5), (N,)) if sampled else np.full(N, 0.5))
+        ploidy = np.full(N, 2.0)
+    else:
+        tau = np.asarray(t_init, dtype=np.float64)
+    out["expose_tau"] = tau
+    mu = reads.astype(np.float64).mean(0) / ((1 + tau) * np.asarray(ploidy, dtype=np.float64))
+    out["expose_u"] = (mu + (mu / 10.0) * _median15(rng, stats.norm.ppf, (N,))) if sampled else mu
+    bm = out["expose_beta_means"] if kind == 1 else np.asarray(beta_means, dtype=np.float64).reshape(n_libs, K1)
+    bs = out["expose_beta_stds"]
+    libs = np.asarray(libs)
+    loc, scale = bm[libs], bs[libs]
+    out["expose_betas"] = (loc + scale * _median15(rng, stats.norm.ppf, (N, K1))) if sampled else loc.copy()
+    return out

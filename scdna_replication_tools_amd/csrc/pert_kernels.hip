@@ -65,7 +65,7 @@ __device__ __forceinline__ float gamma_lp_a(float a) {
 // ------------------------------------------------------------------------------------------
 // Enumerated pass (steps 2/3).  MODE: PERT_MODE_STEP / PERT_MODE_GRAD / PERT_MODE_DECODE.
 template <int P, int MODE>
-__global__ void __launch_bounds__(kBlock) enum_kernel(pert_problem pr, pert_state st,
+__global__ void __launch_bounds__(kBlock, 2) enum_kernel(pert_problem pr, pert_state st,
                                                        pert_adam_hparams hp) {
   constexpr bool kDecode = MODE == PERT_MODE_DECODE;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -103,6 +103,31 @@ __global__ void __launch_bounds__(kBlock) enum_kernel(pert_problem pr, pert_stat
   for (int k = 0; k < PERT_MAX_K1; ++k) acc[k] = 0.0f;
   float accT = 0.0f, loss = 0.0f, ga = 0.0f;
 
+  const float* __restrict__ reads = pr.reads;
+  const uint16_t* __restrict__ codes = pr.eta_code;
+  const float* __restrict__ etab = pr.eta_table;
+  float* __restrict__ zp = st.z_pi;
+  float* __restrict__ mp = st.m_pi;
+  float* __restrict__ vp = st.v_pi;
+  float* __restrict__ gp = st.g_pi;
+
+  // Register software pipeline: the reads / eta code / pi logits of bin l+1 are
+  // loaded while bin l computes (one bin of special-function work hides the HBM
+  // latency); the Adam moments of bin l are loaded at the top of its iteration.
+  float xq = 0.0f;
+  uint32_t cq = 0;
+  float zq[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) zq[k] = 0.0f;
+  if (valid && l0 < l1) {
+    const size_t ln = (size_t)l0 * N + n;
+    const size_t plane = (size_t)l0 * P * N + n;
+    xq = reads[ln];
+    cq = codes[ln];
+#pragma unroll
+    for (int k = 0; k < P; ++k) zq[k] = zp[plane + (size_t)k * N];
+  }
+
   for (int l = l0; l < l1; ++l) {
     float rho;
     if (frozen) {
@@ -117,30 +142,45 @@ __global__ void __launch_bounds__(kBlock) enum_kernel(pert_problem pr, pert_stat
     float gt = 0.0f;
     if (valid) {
       const size_t ln = (size_t)l * N + n;
-      const float x = pr.reads[ln];
-      const float invx = x > 0.0f ? 1.0f / x : 0.0f;
+      const size_t plane = (size_t)l * P * N + n;
+      const float x = xq;
+      const uint32_t code = cq;
+      float z[P];
+#pragma unroll
+      for (int k = 0; k < P; ++k) z[k] = zq[k];
+      if (l + 1 < l1) {
+        xq = reads[ln + N];
+        cq = codes[ln + N];
+#pragma unroll
+        for (int k = 0; k < P; ++k) zq[k] = zp[plane + (size_t)(P + k) * N];
+      }
+      float mm[P], vv[P];
+      if (MODE == PERT_MODE_STEP) {
+#pragma unroll
+        for (int k = 0; k < P; ++k) { mm[k] = mp[plane + (size_t)k * N]; vv[k] = vp[plane + (size_t)k * N]; }
+      }
+      const float invx = x > 0.0f ? frcp(x) : 0.0f;
       float dot = 0.0f;
 #pragma unroll
       for (int k = 0; k < PERT_MAX_K1; ++k) dot += beta[k] * g[k];
       const float omega = fexp(dot);                         // pert_model.py:633
       const float D = ucc * omega;                           // :636-640 (delta = chi D)
       const float t = tau - rho;                             // :616
-      const float phi = 1.0f / (1.0f + fexp(-a_val * t));    // :619
-      const float* row = pr.eta_table + (size_t)pr.eta_code[ln] * (P + 1);
-      float em1[P], z[P];
-#pragma unroll
-      for (int k = 0; k < P; ++k) em1[k] = row[k];
-      const float S1 = row[P];
-      const size_t plane = (size_t)l * P * N + n;
-#pragma unroll
-      for (int k = 0; k < P; ++k) z[k] = st.z_pi[plane + (size_t)k * N];
-      EnumOut<P> o;
-      enum_cellbin<P, !kDecode, kDecode>(x, invx, em1, S1, z, pr.log1m_lam, D, phi, o);
+      const float phi = frcp(1.0f + fexp(-a_val * t));       // :619
+      EnumFwd<P> o;
+      enum_forward<P, !kDecode, kDecode>(x, invx, z, pr.log1m_lam, D, phi, o);
       if (kDecode) {
         st.cn_out[ln] = (uint8_t)(o.argmax % P);
         st.rep_out[ln] = (uint8_t)(o.argmax / P);
       } else {
-        loss += o.E + o.dirv;
+        const float* row = etab + (size_t)code * (P + 1);
+        float em1[P];
+#pragma unroll
+        for (int k = 0; k < P; ++k) em1[k] = row[k];
+        const float S1 = row[P];
+        float gz[P];
+        const float dirv = enum_tail<P>(o, z, em1, S1, gz);
+        loss += o.E + dirv;
         gt = o.gt;
         accT += a_val * o.gt;
         ga += t * o.gt;
@@ -150,19 +190,18 @@ __global__ void __launch_bounds__(kBlock) enum_kernel(pert_problem pr, pert_stat
         if (MODE == PERT_MODE_STEP) {
 #pragma unroll
           for (int k = 0; k < P; ++k) {
+            const float gl = -gz[k];                        // d(-ELBO)/dz
+            const float m1 = hp.beta1 * mm[k] + (1.0f - hp.beta1) * gl;
+            const float v1 = hp.beta2 * vv[k] + (1.0f - hp.beta2) * gl * gl;
+            const float denom = __builtin_sqrtf(v1) * hp.inv_bc2_sqrt + hp.eps;
             const size_t idx = plane + (size_t)k * N;
-            const float gl = -o.gz[k];                      // d(-ELBO)/dz
-            float mm = st.m_pi[idx], vv = st.v_pi[idx];
-            mm = hp.beta1 * mm + (1.0f - hp.beta1) * gl;
-            vv = hp.beta2 * vv + (1.0f - hp.beta2) * gl * gl;
-            const float denom = sqrtf(vv) * hp.inv_bc2_sqrt + hp.eps;
-            st.z_pi[idx] = z[k] - hp.step_size * mm / denom;
-            st.m_pi[idx] = mm;
-            st.v_pi[idx] = vv;
+            zp[idx] = z[k] - hp.step_size * m1 * frcp(denom);
+            mp[idx] = m1;
+            vp[idx] = v1;
           }
         } else {
 #pragma unroll
-          for (int k = 0; k < P; ++k) st.g_pi[plane + (size_t)k * N] = -o.gz[k];
+          for (int k = 0; k < P; ++k) gp[plane + (size_t)k * N] = -gz[k];
         }
       }
     }

@@ -111,20 +111,25 @@ PERT_HD constexpr bool chi_needed(int chi) { return chi < P || (chi % 2) == 0; }
 
 // ----------------------------------------------------------------- enumerated cell.bin
 // One (bin, cell) of the step-2/3 enumerated log joint: forward, responsibilities
-// and the analytic backward.
+// and the analytic backward.  Split in two so a kernel can
+// keep few arrays live: enum_forward needs only the pi logits z; enum_tail adds
+// the Dirichlet terms once eta (em1 = eta - 1, S1 = sum em1) is at hand.
 template <int P>
-struct EnumOut {
+struct EnumFwd {
   float E;        // logsumexp_{c,r} s(c, r)                        (pert_model.py:607-646, B.1)
-  float dirv;     // sum_k (eta_k - 1) log pi_k                     (dirichlet.py:93-97, variable part)
   float gD;       // dE/dD, D = u omega (1-lam)/lam                 (delta = chi D, mask delta >= 1)
   float gt;       // dE/dt / a, t = tau - rho                        (masked where phi clamped)
-  float gz[P];    // d(E + dirv)/dz_k (z = unconstrained pi logits)
-  int   argmax;   // r * P + c of the joint MAP state               (infer_discrete, B.7)
+  float zmax;     // max_k z_k
+  float lse1p;    // log1p(sum_{k != argmax} exp(z_k - zmax)) -> log pi_k = z_k - zmax - lse1p
+  float sgm;      // sum_k gamma^cn_k [pi_k unclamped]
+  float pi[P];    // softmax(z)
+  float gcm[P];   // gamma^cn_k [pi_k unclamped]
+  int argmax;     // r * P + c of the joint MAP state               (infer_discrete, B.7)
 };
 
 template <int P, bool WANT_GRAD, bool WANT_ARGMAX>
-PERT_HD void enum_cellbin(float x, float invx, const float (&em1)[P], float S1, const float (&z)[P],
-                          float log1m_lam, float D, float phi_raw, EnumOut<P>& o) {
+PERT_HD void enum_forward(float x, float invx, const float (&z)[P], float log1m_lam, float D,
+                          float phi_raw, EnumFwd<P>& o) {
   // Bernoulli(phi) with the in-place clamps of pert_model.py:622-623
   float phic = phi_raw;
   bool mphi = true;
@@ -139,62 +144,61 @@ PERT_HD void enum_cellbin(float x, float invx, const float (&em1)[P], float S1, 
   int jmax = 0;
 #pragma unroll
   for (int k = 1; k < P; ++k) { if (z[k] > m) { m = z[k]; jmax = k; } }
-  float e[P];
   float t = 0.0f;
 #pragma unroll
   for (int k = 0; k < P; ++k) {
-    e[k] = (k == jmax) ? 1.0f : fexp(z[k] - m);
-    t += (k == jmax) ? 0.0f : e[k];
+    o.pi[k] = (k == jmax) ? 1.0f : fexp(z[k] - m);
+    t += (k == jmax) ? 0.0f : o.pi[k];
   }
   const float inv1t = frcp(1.0f + t);
   const float lse1p = log1p_corr(t, inv1t);
-  float pi[P], lc[P];
-  bool mk[P];
-  float dirv = 0.0f;
+  o.zmax = m;
+  o.lse1p = lse1p;
+  // joint scores s(c, r): r-major like the oracle's (2, P) layout
+  float s[2 * P];
+  uint32_t mk = 0;
 #pragma unroll
   for (int k = 0; k < P; ++k) {
-    const float logpi = (z[k] - m) - lse1p;
-    pi[k] = e[k] * inv1t;
-    const float om = (k == jmax) ? t * inv1t : 1.0f - pi[k];
+    const float e = o.pi[k];
+    const float pk = e * inv1t;
+    o.pi[k] = pk;
+    const float om = (k == jmax) ? t * inv1t : 1.0f - pk;
     const bool hi = om < kEps32;
-    const bool lo = pi[k] < kEps32;
-    mk[k] = !(hi || lo);
-    lc[k] = hi ? kLog1mEps32 : (lo ? kLogEps32 : logpi);
-    dirv += em1[k] * logpi;
+    const bool lo = pk < kEps32;
+    mk |= (hi || lo) ? 0u : (1u << k);
+    const float lc = hi ? kLog1mEps32 : (lo ? kLogEps32 : (z[k] - m) - lse1p);
+    s[k] = lc + l1mphi;
+    s[P + k] = lc + lphi;
   }
-  o.dirv = dirv;
 
-  // negative-binomial part per distinct chi
+  // negative-binomial part per distinct chi, folded straight into the scores
   float lam1, psi1;
   nb_lgdiff(1.0f, x, invx, lam1, psi1);
   const float n_clamped = log1m_lam + lam1;   // delta == 1 (chi == 0 or chi D < 1)
-  float Nc[2 * P - 1], Bc[2 * P - 1];
-  Nc[0] = n_clamped;
+  float Bc[2 * P - 1];
+  s[0] += n_clamped;
+  s[P] += n_clamped;
   Bc[0] = 0.0f;
 #pragma unroll
   for (int chi = 1; chi < 2 * P - 1; ++chi) {
     if (!chi_needed<P>(chi)) continue;
     const float d = (float)chi * D;
+    float nchi;
     if (d < 1.0f) {
-      Nc[chi] = n_clamped;
+      nchi = n_clamped;
       Bc[chi] = 0.0f;
     } else {
       float lam, psi;
       nb_lgdiff(d, x, invx, lam, psi);
-      Nc[chi] = d * log1m_lam + lam;
+      nchi = d * log1m_lam + lam;
       Bc[chi] = (float)chi * (log1m_lam + psi);
     }
+    if (chi < P) s[chi] += nchi;
+    if ((chi % 2) == 0) s[P + chi / 2] += nchi;
   }
 
-  // joint scores, logsumexp over the 2P states (r-major like the oracle's (2, P) layout)
-  float s[2 * P];
   float smax = -INFINITY;
   int amax = 0;
-#pragma unroll
-  for (int c = 0; c < P; ++c) {
-    s[c] = lc[c] + l1mphi + Nc[c];
-    s[P + c] = lc[c] + lphi + Nc[2 * c];
-  }
 #pragma unroll
   for (int i = 0; i < 2 * P; ++i) { if (s[i] > smax) { smax = s[i]; amax = i; } }
   if (WANT_ARGMAX) o.argmax = amax;
@@ -206,21 +210,52 @@ PERT_HD void enum_cellbin(float x, float invx, const float (&em1)[P], float S1, 
   o.E = smax + flog(se);
 
   float gD = 0.0f, g1 = 0.0f, sgm = 0.0f;
-  float gcn[P];
 #pragma unroll
   for (int c = 0; c < P; ++c) {
     const float g0c = s[c] * inv_se, g1c = s[P + c] * inv_se;
     gD += g0c * Bc[c] + g1c * Bc[2 * c];
     g1 += g1c;
-    gcn[c] = g0c + g1c;
-    sgm += mk[c] ? gcn[c] : 0.0f;
+    const float gm = ((mk >> c) & 1u) ? g0c + g1c : 0.0f;
+    o.gcm[c] = gm;
+    sgm += gm;
   }
   o.gD = gD;
   o.gt = mphi ? (g1 - phic) : 0.0f;
+  o.sgm = sgm;
+}
+
+// Dirichlet(eta) variable part sum_k (eta_k - 1) log pi_k and d(E + dirv)/dz_k, the
+// (eta_k - 1) - pi_k S1 term in the cancellation-free form of SURVEY.md Appendix C.
+template <int P>
+PERT_HD float enum_tail(const EnumFwd<P>& o, const float (&z)[P], const float (&em1)[P], float S1,
+                        float (&gz)[P]) {
+  float dirv = 0.0f;
 #pragma unroll
   for (int k = 0; k < P; ++k) {
-    // (eta_k - 1) - pi_k S1 in the cancellation-free form (Appendix C) + Categorical term
-    o.gz[k] = em1[k] - pi[k] * S1 + (mk[k] ? gcn[k] : 0.0f) - pi[k] * sgm;
+    dirv += em1[k] * ((z[k] - o.zmax) - o.lse1p);
+    gz[k] = em1[k] - o.pi[k] * S1 + o.gcm[k] - o.pi[k] * o.sgm;
+  }
+  return dirv;
+}
+
+template <int P>
+struct EnumOut {
+  float E, dirv, gD, gt;
+  float gz[P];
+  int argmax;
+};
+
+template <int P, bool WANT_GRAD, bool WANT_ARGMAX>
+PERT_HD void enum_cellbin(float x, float invx, const float (&em1)[P], float S1, const float (&z)[P],
+                          float log1m_lam, float D, float phi_raw, EnumOut<P>& out) {
+  EnumFwd<P> o;
+  enum_forward<P, WANT_GRAD, WANT_ARGMAX>(x, invx, z, log1m_lam, D, phi_raw, o);
+  out.E = o.E;
+  out.argmax = WANT_ARGMAX ? o.argmax : 0;
+  if (WANT_GRAD) {
+    out.gD = o.gD;
+    out.gt = o.gt;
+    out.dirv = enum_tail<P>(o, z, em1, S1, out.gz);
   }
 }
 

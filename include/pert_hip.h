@@ -17,14 +17,16 @@
  * positive PERT_E* code for an argument error and 1000 + hipError_t for a launch
  * failure.  A NaN loss is returned as data (pert_model.py:755-758), never raised.
  *
- * Layouts (bin-major like the reference's (loci x cells) tensors, pert_model.py:156-166):
- *   reads      float  [L][N]       integer-valued counts
+ * Layouts (bin-major like the reference's (loci x cells) tensors, pert_model.py:156-166);
+ * ldn = N rounded up to a multiple of 256 (PERT_BLOCK); padded cells are never stored:
+ *   reads      float  [L][ldn]     integer-valued counts
  *   gcf        float  [L][K1]      [gc^K .. gc^1, 1] (make_gc_features, pert_model.py:460-463)
- *   eta_code   uint16 [L][N]       row index into eta_table          (steps 2/3)
+ *   eta_code   uint16 [L][ldn]     row index into eta_table          (steps 2/3)
  *   eta_table  float  [n_codes][P+1]  (eta_k - 1 for k < P, then S1 = sum_k (eta_k - 1))
- *   z_pi/m_pi/v_pi float [L][P][N]  softmax logits of expose_pi + Adam moments, one
- *                                   plane per CN state so lanes (cells) coalesce
- *   cn_obs/rep_obs uint8 [L][N]    step-1 observed states
+ *   z_pi/m_pi/v_pi/g_pi float [L][ldn/64][P][64]  softmax logits of expose_pi and Adam
+ *                                   moments in wave tiles: cell n, state k of bin l at
+ *                                   ((l*(ldn/64) + n/64)*P + k)*64 + n%64
+ *   cn_obs/rep_obs, cn_out/rep_out uint8 [L][ldn]
  *   packed params (unconstrained, see pert_layout below), float
  */
 #ifndef PERT_HIP_H
@@ -74,6 +76,7 @@ typedef struct {
 
 typedef struct {
   int32_t kind, L, N, P, K1, n_libs, n_codes;
+  int32_t ldn;                     /* row stride (cells) of every [L][*] array: N rounded up to 256 */
   int32_t is_root;                 /* adds the global priors once across ranks */
   const float* reads;
   const float* gcf;
@@ -99,11 +102,11 @@ typedef struct {
   float* adam_v;                   /* [n_params] */
   double* grad_shared;             /* [n_shared + 1]: d loss / d shared params, then loss (local sum) */
   float* grad_cell;                /* [n_params - n_shared] */
-  float* z_pi;                     /* [L][P][N] steps 2/3 */
+  float* z_pi;                     /* [L][ldn/64][P][64] steps 2/3 */
   float* m_pi;
   float* v_pi;
-  float* g_pi;                     /* [L][P][N] only for PERT_MODE_GRAD */
-  uint8_t* cn_out;                 /* [L][N] PERT_MODE_DECODE */
+  float* g_pi;                     /* [L][ldn/64][P][64] only for PERT_MODE_GRAD */
+  uint8_t* cn_out;                 /* [L][ldn] PERT_MODE_DECODE */
   uint8_t* rep_out;
   /* workspace, sized by pert_workspace_sizes() */
   float* cell_part;

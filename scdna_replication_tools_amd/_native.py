@@ -39,7 +39,7 @@ class PertLayout(ctypes.Structure):
 class PertProblem(ctypes.Structure):
     _fields_ = [
         ("kind", c_int32), ("L", c_int32), ("N", c_int32), ("P", c_int32), ("K1", c_int32),
-        ("n_libs", c_int32), ("n_codes", c_int32), ("is_root", c_int32),
+        ("n_libs", c_int32), ("n_codes", c_int32), ("ldn", c_int32), ("is_root", c_int32),
         ("reads", c_void_p), ("gcf", c_void_p), ("libs", c_void_p), ("eta_code", c_void_p),
         ("eta_table", c_void_p), ("cn_obs", c_void_p), ("rep_obs", c_void_p),
         ("mean_reads", c_void_p), ("ploidy", c_void_p),

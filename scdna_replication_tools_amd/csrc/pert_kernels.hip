@@ -110,22 +110,29 @@ __global__ void __launch_bounds__(kBlock, 2) enum_kernel(pert_problem pr, pert_s
   float* __restrict__ mp = st.m_pi;
   float* __restrict__ vp = st.v_pi;
   float* __restrict__ gp = st.g_pi;
+  // (L, P, N) state in wave tiles [L][ldn/64][P][64]: one wave's P planes of a bin are
+  // one contiguous P*256-byte run, so a lane needs one address per bin and the planes
+  // are immediate offsets (k * 256 B).
+  const int ldn = pr.ldn;
+  const size_t bin_stride = (size_t)(ldn >> 6) * P * 64;
+  const size_t toff = (size_t)(n >> 6) * P * 64 + lane;
 
   // Register software pipeline: the reads / eta code / pi logits of bin l+1 are
   // loaded while bin l computes (one bin of special-function work hides the HBM
   // latency); the Adam moments of bin l are loaded at the top of its iteration.
+  // Rows are padded to ldn (multiple of 256) so every lane of a launched workgroup
+  // may load; only valid lanes store or accumulate.
   float xq = 0.0f;
   uint32_t cq = 0;
   float zq[P];
 #pragma unroll
   for (int k = 0; k < P; ++k) zq[k] = 0.0f;
-  if (valid && l0 < l1) {
-    const size_t ln = (size_t)l0 * N + n;
-    const size_t plane = (size_t)l0 * P * N + n;
-    xq = reads[ln];
-    cq = codes[ln];
+  if (l0 < l1) {
+    xq = reads[(size_t)l0 * ldn + n];
+    cq = codes[(size_t)l0 * ldn + n];
+    const float* zt = zp + (size_t)l0 * bin_stride + toff;
 #pragma unroll
-    for (int k = 0; k < P; ++k) zq[k] = zp[plane + (size_t)k * N];
+    for (int k = 0; k < P; ++k) zq[k] = zt[k * 64];
   }
 
   for (int l = l0; l < l1; ++l) {
@@ -140,46 +147,51 @@ __global__ void __launch_bounds__(kBlock, 2) enum_kernel(pert_problem pr, pert_s
 #pragma unroll
     for (int k = 0; k < PERT_MAX_K1; ++k) g[k] = (k < K1) ? pr.gcf[l * K1 + k] : 0.0f;
     float gt = 0.0f;
-    if (valid) {
-      const size_t ln = (size_t)l * N + n;
-      const size_t plane = (size_t)l * P * N + n;
-      const float x = xq;
-      const uint32_t code = cq;
-      float z[P];
+    const size_t ln = (size_t)l * ldn + n;
+    const size_t tile = (size_t)l * bin_stride + toff;
+    const float x = xq;
+    const uint32_t code = cq;
+    float z[P];
 #pragma unroll
-      for (int k = 0; k < P; ++k) z[k] = zq[k];
-      if (l + 1 < l1) {
-        xq = reads[ln + N];
-        cq = codes[ln + N];
+    for (int k = 0; k < P; ++k) z[k] = zq[k];
+    if (l + 1 < l1) {
+      xq = reads[ln + ldn];
+      cq = codes[ln + ldn];
+      const float* zt = zp + tile + bin_stride;
 #pragma unroll
-        for (int k = 0; k < P; ++k) zq[k] = zp[plane + (size_t)(P + k) * N];
-      }
-      float mm[P], vv[P];
-      if (MODE == PERT_MODE_STEP) {
+      for (int k = 0; k < P; ++k) zq[k] = zt[k * 64];
+    }
+    float mm[P], vv[P];
+    if (MODE == PERT_MODE_STEP) {
+      const float* mt = mp + tile;
+      const float* vt = vp + tile;
 #pragma unroll
-        for (int k = 0; k < P; ++k) { mm[k] = mp[plane + (size_t)k * N]; vv[k] = vp[plane + (size_t)k * N]; }
-      }
-      const float invx = x > 0.0f ? frcp(x) : 0.0f;
-      float dot = 0.0f;
+      for (int k = 0; k < P; ++k) { mm[k] = mt[k * 64]; vv[k] = vt[k * 64]; }
+    }
+    const float invx = x > 0.0f ? frcp(x) : 0.0f;
+    float dot = 0.0f;
 #pragma unroll
-      for (int k = 0; k < PERT_MAX_K1; ++k) dot += beta[k] * g[k];
-      const float omega = fexp(dot);                         // pert_model.py:633
-      const float D = ucc * omega;                           // :636-640 (delta = chi D)
-      const float t = tau - rho;                             // :616
-      const float phi = frcp(1.0f + fexp(-a_val * t));       // :619
-      EnumFwd<P> o;
-      enum_forward<P, !kDecode, kDecode>(x, invx, z, pr.log1m_lam, D, phi, o);
-      if (kDecode) {
+    for (int k = 0; k < PERT_MAX_K1; ++k) dot += beta[k] * g[k];
+    const float omega = fexp(dot);                         // pert_model.py:633
+    const float D = ucc * omega;                           // :636-640 (delta = chi D)
+    const float t = tau - rho;                             // :616
+    const float phi = frcp(1.0f + fexp(-a_val * t));       // :619
+    EnumFwd<P> o;
+    enum_forward<P, !kDecode, kDecode>(x, invx, z, pr.log1m_lam, D, phi, o);
+    if (kDecode) {
+      if (valid) {
         st.cn_out[ln] = (uint8_t)(o.argmax % P);
         st.rep_out[ln] = (uint8_t)(o.argmax / P);
-      } else {
-        const float* row = etab + (size_t)code * (P + 1);
-        float em1[P];
+      }
+    } else {
+      const float* row = etab + (size_t)code * (P + 1);
+      float em1[P];
 #pragma unroll
-        for (int k = 0; k < P; ++k) em1[k] = row[k];
-        const float S1 = row[P];
-        float gz[P];
-        const float dirv = enum_tail<P>(o, z, em1, S1, gz);
+      for (int k = 0; k < P; ++k) em1[k] = row[k];
+      const float S1 = row[P];
+      float gz[P];
+      const float dirv = enum_tail<P>(o, z, em1, S1, gz);
+      if (valid) {
         loss += o.E + dirv;
         gt = o.gt;
         accT += a_val * o.gt;
@@ -188,20 +200,23 @@ __global__ void __launch_bounds__(kBlock, 2) enum_kernel(pert_problem pr, pert_s
 #pragma unroll
         for (int k = 0; k < PERT_MAX_K1; ++k) acc[k] += ge * g[k];
         if (MODE == PERT_MODE_STEP) {
+          float* zt = zp + tile;
+          float* mt = mp + tile;
+          float* vt = vp + tile;
 #pragma unroll
           for (int k = 0; k < P; ++k) {
             const float gl = -gz[k];                        // d(-ELBO)/dz
             const float m1 = hp.beta1 * mm[k] + (1.0f - hp.beta1) * gl;
             const float v1 = hp.beta2 * vv[k] + (1.0f - hp.beta2) * gl * gl;
             const float denom = __builtin_sqrtf(v1) * hp.inv_bc2_sqrt + hp.eps;
-            const size_t idx = plane + (size_t)k * N;
-            zp[idx] = z[k] - hp.step_size * m1 * frcp(denom);
-            mp[idx] = m1;
-            vp[idx] = v1;
+            zt[k * 64] = z[k] - hp.step_size * m1 * frcp(denom);
+            mt[k * 64] = m1;
+            vt[k * 64] = v1;
           }
         } else {
+          float* gt_ = gp + tile;
 #pragma unroll
-          for (int k = 0; k < P; ++k) gp[plane + (size_t)k * N] = -gz[k];
+          for (int k = 0; k < P; ++k) gt_[k * 64] = -gz[k];
         }
       }
     }
@@ -284,7 +299,7 @@ __global__ void __launch_bounds__(kBlock) obs_kernel(pert_problem pr, pert_state
     for (int k = 0; k < PERT_MAX_K1; ++k) g[k] = (k < K1) ? pr.gcf[l * K1 + k] : 0.0f;
     float gt = 0.0f;
     if (valid) {
-      const size_t ln = (size_t)l * N + n;
+      const size_t ln = (size_t)l * pr.ldn + n;
       const float x = pr.reads[ln];
       const float invx = x > 0.0f ? 1.0f / x : 0.0f;
       float dot = 0.0f;
@@ -362,9 +377,12 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(pert_problem pr, pert_
     return;
   }
 
-  // ---- per-cell
-  const int n = blockIdx.x * kBlock + tid;
-  const bool valid = n < N;
+  // ---- per-cell: 64 cells per workgroup; the 4 waves split the bin tiles, then LDS
+  __shared__ double s_acc[kWaves][PERT_MAX_K1 + 1][64];
+  const int cl = tid & 63, grp = tid >> 6;
+  const int n = blockIdx.x * 64 + cl;
+  const bool in_range = n < N;
+  const bool valid = in_range && grp == 0;
   float lam = pr.lamb;
   if (step1) {
     float dml;
@@ -376,16 +394,32 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(pert_problem pr, pert_
   int lib = 0;
 #pragma unroll
   for (int k = 0; k < PERT_MAX_K1; ++k) { dzbs[k] = 0.0f; dbm[k] = 0.0f; }
+  {
+    double A[PERT_MAX_K1 + 1];
+#pragma unroll
+    for (int k = 0; k <= PERT_MAX_K1; ++k) A[k] = 0.0;
+    if (in_range) {
+      for (int bt = grp; bt < n_bt; bt += kWaves) {
+        const float* cp = st.cell_part + (size_t)bt * (K1 + 1) * N + n;
+#pragma unroll
+        for (int k = 0; k <= PERT_MAX_K1; ++k)
+          if (k <= K1) A[k] += (double)cp[(size_t)k * N];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k <= PERT_MAX_K1; ++k) s_acc[grp][k][cl] = A[k];
+  }
+  __syncthreads();
   if (valid) {
     double A[PERT_MAX_K1], T = 0.0;
 #pragma unroll
     for (int k = 0; k < PERT_MAX_K1; ++k) A[k] = 0.0;
-    for (int bt = 0; bt < n_bt; ++bt) {
-      const float* cp = st.cell_part + (size_t)bt * (K1 + 1) * N + n;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
 #pragma unroll
       for (int k = 0; k < PERT_MAX_K1; ++k)
-        if (k < K1) A[k] += (double)cp[(size_t)k * N];
-      T += (double)cp[(size_t)K1 * N];
+        if (k < K1) A[k] += s_acc[w][k][cl];
+      T += s_acc[w][K1][cl];
     }
     const float u = st.params[lay.off_u + n];
     float dtau_dz;
@@ -574,7 +608,8 @@ int tile_bins(const pert_state* st) {
 }
 
 bool problem_ok(const pert_problem* p) {
-  return p && p->L > 0 && p->N > 0 && p->K1 >= 1 && p->K1 <= PERT_MAX_K1 && p->n_libs >= 1 &&
+  return p && p->L > 0 && p->N > 0 && p->ldn >= p->N && p->ldn % PERT_BLOCK == 0 &&
+         p->K1 >= 1 && p->K1 <= PERT_MAX_K1 && p->n_libs >= 1 &&
          p->P >= PERT_MIN_P && p->P <= PERT_MAX_P && p->reads && p->gcf && p->libs && p->mean_reads &&
          p->ploidy;
 }
@@ -644,7 +679,7 @@ int pert_workspace_sizes(int32_t kind, int32_t L, int32_t N, int32_t K1, int32_t
   if (n_cell_part) *n_cell_part = n_bt * (K1 + 1) * (int64_t)N;
   if (n_bin_part) *n_bin_part = n_ct * (int64_t)L;
   if (n_blk_part) *n_blk_part = n_bt * n_ct * kBlkSlots;
-  if (n_cellblk_part) *n_cellblk_part = n_ct * (2 * (int64_t)n_libs * K1 + 1);
+  if (n_cellblk_part) *n_cellblk_part = ((N + 63) / 64) * (2 * (int64_t)n_libs * K1 + 1);
   return PERT_OK;
 }
 
@@ -689,11 +724,12 @@ int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream) 
   const int n_ct = (prob->N + kBlock - 1) / kBlock;
   const int n_bt = (prob->L + lt - 1) / lt;
   const int n_lblk = (prob->L + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(finalize_kernel, dim3(n_ct + n_lblk), dim3(kBlock), 0, stream, *prob, s2, n_ct,
+  const int n_cblk = (prob->N + 63) / 64;
+  hipLaunchKernelGGL(finalize_kernel, dim3(n_cblk + n_lblk), dim3(kBlock), 0, stream, *prob, s2, n_cblk,
                      n_bt, n_ct);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_status(e);
-  hipLaunchKernelGGL(scalar_kernel, dim3(1), dim3(kBlock), 0, stream, *prob, s2, n_bt * n_ct, n_ct);
+  hipLaunchKernelGGL(scalar_kernel, dim3(1), dim3(kBlock), 0, stream, *prob, s2, n_bt * n_ct, n_cblk);
   return hip_status(hipGetLastError());
 }
 

@@ -197,9 +197,10 @@ class PertShard:
         self.t = 0
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
+        self.ldn = ldn = -(-N // nat.BLOCK) * nat.BLOCK       # row stride: N rounded up to 256
 
         # ---- inputs (pert_model.py:133-191 layouts)
-        self.reads = torch.as_tensor(reads.astype(F32), device=dev).contiguous()
+        self.reads = self._pad_rows(torch.as_tensor(reads.astype(F32)), dev)
         self.gcf = gc_features(gc, self.K).to(dev).contiguous()
         self.libs = torch.as_tensor(np.asarray(libs).astype(np.int32), device=dev)
         x64 = reads.astype(np.float64)
@@ -224,10 +225,11 @@ class PertShard:
             cn = np.asarray(cn_obs)
             if cn.min() < 0 or cn.max() >= self.P:
                 raise ValueError("observed CN states must lie in [0, P)")
-            self.cn_obs = torch.as_tensor(cn.astype(np.uint8), device=dev).contiguous()
-            self.rep_obs = torch.as_tensor(np.asarray(rep_obs).astype(np.uint8), device=dev).contiguous()
+            self.cn_obs = self._pad_rows(torch.as_tensor(cn.astype(np.uint8)), dev)
+            self.rep_obs = self._pad_rows(torch.as_tensor(np.asarray(rep_obs).astype(np.uint8)), dev)
         else:
-            self.eta_code = torch.as_tensor(np.ascontiguousarray(eta.codes, dtype=np.uint16).view(np.int16), device=dev)
+            self.eta_code = self._pad_rows(
+                torch.as_tensor(np.ascontiguousarray(eta.codes, dtype=np.uint16).view(np.int16)), dev)
             self.eta_table = torch.as_tensor(eta.kernel_table(), device=dev).contiguous()
             lam_f = float(np.asarray(lamb, dtype=F32).reshape(-1)[0])
             self.beta_means_t = torch.as_tensor(np.asarray(beta_means, dtype=F32).reshape(self.n_libs, self.K1),
@@ -252,14 +254,14 @@ class PertShard:
             if pi_init is None:
                 # AutoDelta init of the multivariate Dirichlet site: transform_to(simplex)(0) -> 1/P
                 z0 = float(torch.log(torch.tensor(1.0 / self.P, dtype=torch.float32)))
-                self.z_pi = torch.full((L, self.P, N), z0, **f32)
+                self.z_pi = torch.full((L, ldn // 64, self.P, 64), z0, **f32)
             else:
                 pi0 = torch.as_tensor(np.asarray(pi_init), dtype=torch.float32)
-                self.z_pi = pi0.log().permute(0, 2, 1).contiguous().to(dev)              # SoftmaxTransform.inv
+                self.z_pi = self.to_tiles(pi0.log())                                   # SoftmaxTransform.inv
             self.m_pi = torch.zeros_like(self.z_pi)
             self.v_pi = torch.zeros_like(self.z_pi)
-        self.cn_out = torch.zeros((L, N), dtype=torch.uint8, device=dev)
-        self.rep_out = torch.zeros((L, N), dtype=torch.uint8, device=dev)
+        self.cn_out = torch.zeros((L, ldn), dtype=torch.uint8, device=dev)
+        self.rep_out = torch.zeros((L, ldn), dtype=torch.uint8, device=dev)
 
         ncp, nbp, nblk, ncb = nat.workspace_sizes(self.kind, L, N, self.K1, self.n_libs, bins_per_tile)
         self.cell_part = torch.zeros(ncp, **f32)
@@ -286,7 +288,7 @@ class PertShard:
         # ---- C structs
         self._prob = nat.PertProblem(
             kind=self.kind, L=L, N=N, P=self.P, K1=self.K1, n_libs=self.n_libs,
-            n_codes=0 if eta is None else int(eta.table.shape[0]), is_root=1 if is_root else 0,
+            n_codes=0 if eta is None else int(eta.table.shape[0]), ldn=ldn, is_root=1 if is_root else 0,
             reads=_ptr(self.reads), gcf=_ptr(self.gcf), libs=_ptr(self.libs), eta_code=_ptr(self.eta_code),
             eta_table=_ptr(self.eta_table), cn_obs=_ptr(self.cn_obs), rep_obs=_ptr(self.rep_obs),
             mean_reads=_ptr(self.mean_reads), ploidy=_ptr(self.ploidy), lamb=lam_f,
@@ -302,6 +304,25 @@ class PertShard:
             bins_per_tile=self.bins_per_tile)
         self._hp = nat.PertAdamHparams(lr=self.lr, beta1=self.betas[0], beta2=self.betas[1], eps=self.eps,
                                        step_size=0.0, inv_bc2_sqrt=0.0)
+
+    # ------------------------------------------------------------------ layouts
+    def _pad_rows(self, a: torch.Tensor, dev) -> torch.Tensor:
+        """(L, N) -> (L, ldn) zero-padded device copy (include/pert_hip.h row stride)."""
+        out = torch.zeros((a.shape[0], self.ldn), dtype=a.dtype)
+        out[:, :a.shape[1]] = a
+        return out.to(dev).contiguous()
+
+    def to_tiles(self, a: torch.Tensor) -> torch.Tensor:
+        """(L, N, P) -> wave tiles (L, ldn/64, P, 64) on the device."""
+        L, N, P = a.shape
+        pad = torch.zeros((L, self.ldn, P), dtype=a.dtype)
+        pad[:, :N] = a
+        return pad.reshape(L, self.ldn // 64, 64, P).permute(0, 1, 3, 2).contiguous().to(self.device)
+
+    def from_tiles(self, t: torch.Tensor) -> torch.Tensor:
+        """Wave tiles (L, ldn/64, P, 64) -> (L, N, P)."""
+        L = t.shape[0]
+        return t.permute(0, 1, 3, 2).reshape(L, self.ldn, self.P)[:, :self.N]
 
     # ------------------------------------------------------------------ params
     def _load_init(self, init: Dict[str, np.ndarray]):
@@ -344,7 +365,7 @@ class PertShard:
         p[lay.off_tau:lay.off_tau + N] = t32(z["expose_tau"]).reshape(N)
         self.params.copy_(p.to(self.device))
         if "expose_pi" in z and self.z_pi is not None:
-            self.z_pi.copy_(t32(z["expose_pi"]).permute(0, 2, 1).contiguous().to(self.device))
+            self.z_pi.copy_(self.to_tiles(t32(z["expose_pi"])))
 
     def constrained(self) -> Dict[str, np.ndarray]:
         """Current constrained site values (what the reference's trace exposes)."""
@@ -365,7 +386,7 @@ class PertShard:
 
     def pi(self) -> torch.Tensor:
         """Constrained pi (L, N, P) on the device (SoftmaxTransform of the logits)."""
-        return torch.softmax(self.z_pi, dim=1).permute(0, 2, 1)
+        return self.from_tiles(torch.softmax(self.z_pi, dim=2))
 
     # ------------------------------------------------------------------ launches
     def _stream(self) -> int:
@@ -450,7 +471,7 @@ class PertShard:
         g["expose_betas"] = gc[lay.off_beta - off:lay.off_beta - off + K1 * N].reshape(K1, N).T
         g["expose_tau"] = gc[lay.off_tau - off:lay.off_tau - off + N]
         if self.kind != nat.KIND_STEP1:
-            g["expose_pi"] = self.g_pi.permute(0, 2, 1).cpu().numpy()
+            g["expose_pi"] = self.from_tiles(self.g_pi).cpu().numpy()
         loss = float(gs[lay.n_shared]) - self.const_total
         if self.pi_block is not None:
             lp, gpi = self.pi_block.logp_and_grad()
@@ -462,4 +483,4 @@ class PertShard:
         if self.kind == nat.KIND_STEP1:
             raise ValueError("step 1 has no latent discrete sites")
         self._pass(nat.MODE_DECODE)
-        return self.cn_out, self.rep_out
+        return self.cn_out[:, :self.N], self.rep_out[:, :self.N]

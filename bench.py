@@ -110,6 +110,7 @@ def main():
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     ap.add_argument("--bins-per-tile", type=int, default=0)
+    ap.add_argument("--variant", type=int, default=0, help="enumerated-pass kernel: 0 LDS-DMA, 1 register")
     ap.add_argument("--cpu-cells", type=int, default=128)
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -148,7 +149,7 @@ def main():
     allreduce = (lambda t: pg.all_reduce(t)) if pg is not None else None
     shard = PertShard(2, reads, data["gc"], np.zeros(n1 - n0, int), 1, P, K, init, eta=eta, lamb=0.75,
                       beta_means=bm, device=device, is_root=(rank == 0), n_cells_total=n_total,
-                      allreduce=allreduce, bins_per_tile=args.bins_per_tile)
+                      allreduce=allreduce, bins_per_tile=args.bins_per_tile, variant=args.variant)
     del data
     torch.cuda.synchronize()
 
@@ -196,7 +197,8 @@ def main():
                        "K": K, "cn_prior": "g1_clones (weight 1e6)", "parallelism": "cell-sharded x{}".format(world)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "enum_kernel<13, STEP>", "kernel_ms": kern_ms,
+                         "kernel": ("enum_dma_kernel<13, STEP, 5>" if args.variant == 0 else "enum_kernel<13, STEP>"),
+                         "kernel_ms": kern_ms,
                          "bytes_per_cellbin": bpc},
             "loss_first": losses[0], "loss_last": losses[-1],
         }

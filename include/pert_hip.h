@@ -114,6 +114,7 @@ typedef struct {
   double* blk_part;
   double* cellblk_part;
   int32_t bins_per_tile;           /* LT; 0 = library default */
+  int32_t variant;                 /* enumerated-pass kernel: 0 LDS-DMA streamed (default), 1 register pipelined */
 } pert_state;
 
 typedef struct {

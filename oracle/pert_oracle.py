@@ -389,7 +389,7 @@ def fit(prob: OracleProblem, z0: Dict[str, torch.Tensor], lr: float = 0.05, max_
         if cell_chunk is None:
             loss = -elbo(prob, params)
             loss.backward()
-            lval = float(loss)
+            lval = float(loss.detach())
         else:
             lval = _chunked_backward(prob, params, cell_chunk, ploidy)
         opt.step()
@@ -427,7 +427,7 @@ def _chunked_backward(prob: OracleProblem, params, cell_chunk: int, ploidy) -> f
         terms = model_terms(sub, c, global_terms=(j == 0), ploidy=ploidy[sl])
         loss = -sum(terms.values())
         loss.backward()
-        total += float(loss)
+        total += float(loss.detach())
     return total
 
 

@@ -57,7 +57,7 @@ class PertState(ctypes.Structure):
         ("cn_out", c_void_p), ("rep_out", c_void_p),
         ("cell_part", c_void_p), ("bin_part", c_void_p), ("blk_part", c_void_p),
         ("cellblk_part", c_void_p),
-        ("bins_per_tile", c_int32),
+        ("bins_per_tile", c_int32), ("variant", c_int32),
     ]
 
 

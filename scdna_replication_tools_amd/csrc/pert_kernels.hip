@@ -253,6 +253,224 @@ __global__ void __launch_bounds__(kBlock, 2) enum_kernel(pert_problem pr, pert_s
 }
 
 // ------------------------------------------------------------------------------------------
+// Enumerated pass, LDS-DMA streamed (default).  One wave per workgroup = 64 cells x LT bins.
+// Per bin the wave's inputs are contiguous runs in HBM (x 256 B, eta code 128 B, pi logits
+// and Adam moments P*256 B each in the wave-tiled layout) and are copied HBM -> LDS by
+// global_load_lds (no VGPRs): the inputs of bin l+1 and the Adam moments of bin l are
+// in flight while bin l computes.  LDS-DMA completion is ordered for the issuing wave
+// by its own vmcnt only (no workgroup barrier is needed with one wave), and hipcc does
+// not wait for it on its own, so every wait below is explicit and counted.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+template <int BYTES>
+__device__ __forceinline__ void dma_run(const void* gsrc, float* ldst, int lane) {
+  // a contiguous run of BYTES (multiple of 128) -> the same bytes at ldst
+  const char* g = (const char*)gsrc;
+  constexpr int n16 = BYTES / 1024;
+  constexpr int rem = BYTES % 1024;
+#pragma unroll
+  for (int i = 0; i < n16; ++i)
+    __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g + i * 1024 + lane * 16), (lds_ptr_t)(ldst + i * 256), 16, 0, 0);
+  if constexpr (rem >= 256) {
+#pragma unroll
+    for (int i = 0; i < rem / 256; ++i)
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g + n16 * 1024 + i * 256 + lane * 4),
+                                       (lds_ptr_t)(ldst + n16 * 256 + i * 64), 4, 0, 0);
+  }
+  if constexpr (rem % 256 == 128) {
+    // 128-B tail: 4-B pieces on half the wave (sub-dword LDS-DMA is not lane-packed)
+    if (lane < 32)
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g + BYTES - 128 + lane * 4), (lds_ptr_t)(ldst + (BYTES - 128) / 4), 4, 0, 0);
+  }
+}
+
+template <int BYTES>
+constexpr int dma_count() { return BYTES / 1024 + (BYTES % 1024) / 256 + ((BYTES % 256) == 128 ? 1 : 0); }
+
+template <int P, int MODE, int K1T>
+__global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_state st, pert_adam_hparams hp) {
+  constexpr bool kDecode = MODE == PERT_MODE_DECODE;
+  constexpr bool kStep = MODE == PERT_MODE_STEP;
+  constexpr int ZF = P * 64;                 // floats of one P-plane run
+  constexpr int SF = ZF + 64 + 32;           // stage: z, x, code (64 x u16)
+  constexpr int kStores = kStep ? 3 * P : (kDecode ? 2 : P);   // VMEM stores per iteration
+  // one dynamic LDS array (16-B aligned base, cdna_hip_programming.md G17):
+  //   [stage 0 | stage 1 | m | v (STEP)] [per-bin rho partials: LT] [per-bin rho, gcf: LT x (K1+1)]
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* s_binp = lds + 2 * SF + (kStep ? 2 * ZF : 0);
+
+  const int lane = threadIdx.x;
+  const int N = pr.N, K1 = (K1T == PERT_MAX_K1) ? pr.K1 : K1T, ldn = pr.ldn;
+  const int wt = blockIdx.x;
+  const int n = wt * 64 + lane;
+  const bool valid = n < N;
+  const int LT = st.bins_per_tile;
+  const int l0 = blockIdx.y * LT;
+  const int l1 = min(pr.L, l0 + LT);
+  const bool frozen = pr.kind == PERT_KIND_STEP3;
+  const pert_layout lay = st.lay;
+  const size_t bin_stride = (size_t)(ldn >> 6) * P * 64;     // floats per bin of the tiled state
+  const size_t toff = (size_t)wt * P * 64;
+
+  const float* __restrict__ params = st.params;
+  float* s_bc = s_binp + LT;
+  // per-bin constants of the tile: constrained rho and the GC features
+  for (int i = lane; i < (l1 - l0) * (K1 + 1); i += 64) {
+    const int lb = i / (K1 + 1), j = i - lb * (K1 + 1);
+    float v;
+    if (j == 0) {
+      float dm;
+      v = frozen ? pr.rho_fixed[l0 + lb] : clipped_sigmoid(params[lay.off_rho + l0 + lb], &dm);
+    } else {
+      v = pr.gcf[(l0 + lb) * K1 + j - 1];
+    }
+    s_bc[i] = v;
+  }
+  const float a_val = frozen ? pr.a_fixed : fexp(params[lay.off_a]);
+  const float c0 = (1.0f - pr.lamb) / pr.lamb;
+  float u = 0.0f, tau = 0.5f;
+  float beta[K1T];
+#pragma unroll
+  for (int k = 0; k < K1T; ++k) beta[k] = 0.0f;
+  if (valid) {
+    u = st.params[lay.off_u + n];
+#pragma unroll
+    for (int k = 0; k < K1T; ++k)
+      if (k < K1) beta[k] = st.params[lay.off_beta + k * N + n];
+    float dm;
+    tau = clipped_sigmoid(st.params[lay.off_tau + n], &dm);
+  }
+  const float ucc = u * c0;
+  float acc[K1T];
+#pragma unroll
+  for (int k = 0; k < K1T; ++k) acc[k] = 0.0f;
+  float accT = 0.0f, loss = 0.0f, ga = 0.0f;
+
+  auto issue_stage = [&](int l, int buf) {
+    float* sb = lds + buf * SF;
+    dma_run<P * 256>(st.z_pi + (size_t)l * bin_stride + toff, sb, lane);
+    dma_run<256>(pr.reads + (size_t)l * ldn + wt * 64, sb + ZF, lane);
+    dma_run<128>(pr.eta_code + (size_t)l * ldn + wt * 64, sb + ZF + 64, lane);
+  };
+  if (l0 < l1) issue_stage(l0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  for (int l = l0; l < l1; ++l) {
+    const int buf = (l - l0) & 1;
+    // stage(l) was issued one iteration ago; only this wave's stores of bin l-1
+    // (kStores, unconditional) may be younger than it
+    if (l > l0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(kStores) : "memory");
+    const float* sb = lds + buf * SF;
+    float z[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) z[k] = sb[k * 64 + lane];
+    const float x = sb[ZF + lane];
+    const uint32_t code = ((const uint16_t*)(sb + ZF + 64))[lane];
+    // per-bin constants, read before this iteration's DMAs are issued (hipcc waits for
+    // every outstanding LDS-DMA before the first LDS read that follows one)
+    const float* bcl = s_bc + (l - l0) * (K1 + 1);
+    const float rho = bcl[0];
+    float g[K1T];
+#pragma unroll
+    for (int k = 0; k < K1T; ++k) g[k] = (k < K1) ? bcl[1 + k] : 0.0f;
+    const size_t tile = (size_t)l * bin_stride + toff;
+    if (kStep) {
+      dma_run<P * 256>(st.m_pi + tile, lds + 2 * SF, lane);
+      dma_run<P * 256>(st.v_pi + tile, lds + 2 * SF + ZF, lane);
+    }
+    if (l + 1 < l1) issue_stage(l + 1, buf ^ 1);
+
+    const float invx = x > 0.0f ? frcp(x) : 0.0f;
+    float dot = 0.0f;
+#pragma unroll
+    for (int k = 0; k < K1T; ++k) dot += beta[k] * g[k];
+    const float omega = fexp(dot);                         // pert_model.py:633
+    const float D = ucc * omega;                           // :636-640 (delta = chi D)
+    const float t = tau - rho;                             // :616
+    const float phi = frcp(1.0f + fexp(-a_val * t));       // :619
+    EnumFwd<P> o;
+    enum_forward<P, !kDecode, kDecode>(x, invx, z, pr.log1m_lam, D, phi, o);
+    float gtv = 0.0f;
+    if (kDecode) {
+      st.cn_out[(size_t)l * ldn + n] = (uint8_t)(o.argmax % P);
+      st.rep_out[(size_t)l * ldn + n] = (uint8_t)(o.argmax / P);
+    } else {
+      // Everything the tail needs is re-read from LDS after this point (the asm is a
+      // compiler memory barrier, so the pi logits are not kept live through the NB work).
+      // (the register operand pins the wait after the whole forward pass)
+      if (kStep) asm volatile("s_waitcnt vmcnt(0)" :: "v"(o.E), "v"(o.sgm) : "memory");   // m, v of bin l landed
+      else asm volatile("" :: "v"(o.E), "v"(o.sgm) : "memory");
+      float zt[P];
+#pragma unroll
+      for (int k = 0; k < P; ++k) zt[k] = sb[k * 64 + lane];
+      const float* row = pr.eta_table + (size_t)code * (P + 1);
+      float em1[P];
+#pragma unroll
+      for (int k = 0; k < P; ++k) em1[k] = row[k];
+      const float S1 = row[P];
+      float gz[P];
+      const float dirv = enum_tail<P>(o, zt, em1, S1, gz);
+      if (valid) {
+        loss += o.E + dirv;
+        gtv = o.gt;
+        accT += a_val * o.gt;
+        ga += t * o.gt;
+        const float ge = o.gD * omega;
+#pragma unroll
+        for (int k = 0; k < K1T; ++k) acc[k] += ge * g[k];
+      }
+      if (kStep) {
+        const float* mb = lds + 2 * SF;
+        float* zo = st.z_pi + tile + lane;
+        float* mo = st.m_pi + tile + lane;
+        float* vo = st.v_pi + tile + lane;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+          const float gl = -gz[k];                          // d(-ELBO)/dz
+          const float m1 = hp.beta1 * mb[k * 64 + lane] + (1.0f - hp.beta1) * gl;
+          const float v1 = hp.beta2 * mb[ZF + k * 64 + lane] + (1.0f - hp.beta2) * gl * gl;
+          const float denom = __builtin_sqrtf(v1) * hp.inv_bc2_sqrt + hp.eps;
+          zo[k * 64] = zt[k] - hp.step_size * m1 * frcp(denom);
+          mo[k * 64] = m1;
+          vo[k * 64] = v1;
+        }
+      } else {
+        float* gp = st.g_pi + tile + lane;
+#pragma unroll
+        for (int k = 0; k < P; ++k) gp[k * 64] = -gz[k];
+      }
+    }
+    if (!kDecode && !frozen) {
+      const float ws = wave_sum(gtv);
+      if (lane == 0) s_binp[l - l0] = ws;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (kDecode) return;
+  __syncthreads();
+  if (!frozen) {
+    for (int i = lane; i < l1 - l0; i += 64) st.bin_part[(size_t)wt * pr.L + l0 + i] = s_binp[i];
+  }
+  if (valid) {
+    float* cp = st.cell_part + (size_t)blockIdx.y * (K1 + 1) * N + n;
+#pragma unroll
+    for (int k = 0; k < K1T; ++k)
+      if (k < K1) cp[(size_t)k * N] = acc[k];
+    cp[(size_t)K1 * N] = accT;
+  }
+  const double bl = wave_sum_d((double)loss);
+  const double bga = wave_sum_d((double)ga);
+  if (lane == 0) {
+    double* bp = st.blk_part + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlkSlots;
+    bp[0] = bl;
+    bp[1] = bga;
+    bp[2] = 0.0;
+    bp[3] = 0.0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Observed pass (step 1): cn, rep conditioned (pert_model.py:724-729).
 __global__ void __launch_bounds__(kBlock) obs_kernel(pert_problem pr, pert_state st) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -614,12 +832,28 @@ bool problem_ok(const pert_problem* p) {
          p->ploidy;
 }
 
+size_t dma_lds_bytes(int P, int mode, const pert_state& st, const pert_problem& pr) {
+  const int ZF = P * 64, SF = ZF + 96;
+  const int lt = st.bins_per_tile;
+  return sizeof(float) * (size_t)(2 * SF + (mode == PERT_MODE_STEP ? 2 * ZF : 0) + lt + lt * (pr.K1 + 1));
+}
+
+// cells per tile of the enumerated pass: 64 for the LDS-DMA kernel (variant 0), 256 otherwise
+int enum_cell_tile(const pert_state* st) { return st->variant == 0 ? 64 : kBlock; }
+
 template <int MODE>
 int launch_enum_mode(int P, dim3 grid, const pert_problem& pr, const pert_state& st,
                      const pert_adam_hparams& hp, hipStream_t s) {
+  const bool dma = st.variant == 0;
   switch (P) {
-#define PERT_CASE(PP) \
-  case PP: hipLaunchKernelGGL((enum_kernel<PP, MODE>), grid, dim3(kBlock), 0, s, pr, st, hp); break;
+#define PERT_CASE(PP)                                                                             \
+  case PP:                                                                                        \
+    if (dma && pr.K1 == 5)                                                                        \
+      hipLaunchKernelGGL((enum_dma_kernel<PP, MODE, 5>), grid, dim3(64), dma_lds_bytes(PP, MODE, st, pr), s, pr, st, hp); \
+    else if (dma)                                                                                 \
+      hipLaunchKernelGGL((enum_dma_kernel<PP, MODE, PERT_MAX_K1>), grid, dim3(64), dma_lds_bytes(PP, MODE, st, pr), s, pr, st, hp); \
+    else hipLaunchKernelGGL((enum_kernel<PP, MODE>), grid, dim3(kBlock), 0, s, pr, st, hp);       \
+    break;
     PERT_CASE(2) PERT_CASE(3) PERT_CASE(4) PERT_CASE(5) PERT_CASE(6) PERT_CASE(7) PERT_CASE(8)
     PERT_CASE(9) PERT_CASE(10) PERT_CASE(11) PERT_CASE(12) PERT_CASE(13) PERT_CASE(14)
     PERT_CASE(15) PERT_CASE(16)
@@ -675,7 +909,8 @@ int pert_workspace_sizes(int32_t kind, int32_t L, int32_t N, int32_t K1, int32_t
   pert_state tmp;
   tmp.bins_per_tile = bins_per_tile;
   const int lt = tile_bins(&tmp);
-  const int64_t n_bt = (L + lt - 1) / lt, n_ct = (N + kBlock - 1) / kBlock;
+  const int64_t ldn = (N + kBlock - 1) / kBlock * kBlock;
+  const int64_t n_bt = (L + lt - 1) / lt, n_ct = ldn / 64;     // sized for the 64-cell tiles
   if (n_cell_part) *n_cell_part = n_bt * (K1 + 1) * (int64_t)N;
   if (n_bin_part) *n_bin_part = n_ct * (int64_t)L;
   if (n_blk_part) *n_blk_part = n_bt * n_ct * kBlkSlots;
@@ -697,7 +932,8 @@ int pert_enum_pass(const pert_problem* prob, pert_state* st, const pert_adam_hpa
     return PERT_E_ARG;
   pert_state s2 = *st;
   s2.bins_per_tile = tile_bins(st);
-  const dim3 grid((prob->N + kBlock - 1) / kBlock, (prob->L + s2.bins_per_tile - 1) / s2.bins_per_tile);
+  const int ct = enum_cell_tile(st);
+  const dim3 grid(prob->ldn / ct, (prob->L + s2.bins_per_tile - 1) / s2.bins_per_tile);
   switch (mode) {
     case PERT_MODE_STEP: return launch_enum_mode<PERT_MODE_STEP>(prob->P, grid, *prob, s2, *hp, stream);
     case PERT_MODE_GRAD: return launch_enum_mode<PERT_MODE_GRAD>(prob->P, grid, *prob, s2, *hp, stream);
@@ -721,7 +957,8 @@ int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream) 
   pert_state s2 = *st;
   s2.bins_per_tile = tile_bins(st);
   const int lt = s2.bins_per_tile;
-  const int n_ct = (prob->N + kBlock - 1) / kBlock;
+  const int ct = prob->kind == PERT_KIND_STEP1 ? kBlock : enum_cell_tile(st);
+  const int n_ct = prob->ldn / ct;
   const int n_bt = (prob->L + lt - 1) / lt;
   const int n_lblk = (prob->L + kBlock - 1) / kBlock;
   const int n_cblk = (prob->N + 63) / 64;

@@ -151,7 +151,7 @@ class CanonicalPiBlock:
         p = p / p.sum()
         lp = torch.log(torch.clamp(p, min=EPS32, max=1 - EPS32))[0]   # observed state at index 0
         lp.backward()
-        return float(lp), (-z.grad).numpy().astype(F32)             # loss gradient
+        return float(lp.detach()), (-z.grad).numpy().astype(F32)             # loss gradient
 
     def step(self, t: int) -> float:
         lp, g = self.logp_and_grad()
@@ -178,7 +178,7 @@ class PertShard:
                  pi_init=None, device=None, lr: float = 0.05, betas=ADAM_BETAS, eps: float = ADAM_EPS,
                  is_root: bool = True, n_cells_total: Optional[int] = None,
                  allreduce: Optional[Callable[[torch.Tensor], None]] = None,
-                 dirichlet_mode: str = "torch32", bins_per_tile: int = 0):
+                 dirichlet_mode: str = "torch32", bins_per_tile: int = 0, variant: int = 0):
         self.lib = nat.lib()
         self.kind = int(kind)
         self.device = torch.device(device if device is not None else "cuda")
@@ -301,7 +301,7 @@ class PertShard:
             m_pi=_ptr(self.m_pi), v_pi=_ptr(self.v_pi), g_pi=0, cn_out=_ptr(self.cn_out),
             rep_out=_ptr(self.rep_out), cell_part=_ptr(self.cell_part), bin_part=_ptr(self.bin_part),
             blk_part=_ptr(self.blk_part), cellblk_part=_ptr(self.cellblk_part),
-            bins_per_tile=self.bins_per_tile)
+            bins_per_tile=self.bins_per_tile, variant=int(variant))
         self._hp = nat.PertAdamHparams(lr=self.lr, beta1=self.betas[0], beta2=self.betas[1], eps=self.eps,
                                        step_size=0.0, inv_bc2_sqrt=0.0)
 

@@ -1,0 +1,349 @@
+"""Host-side input preparation of the PERT fit, vectorised (no per-cell Python loops
+over the long-form tables).
+
+Mirrors, with identical outputs on complete inputs:
+  * ``pert_infer_scRT.process_input_data`` / ``sort_by_cell_and_loci`` /
+    ``get_libraries_tensor`` (reference pert_model.py:133-225)
+  * ``compute_consensus_clone_profiles`` + ``add_cell_ploidies`` + ``filter_ploidies``
+    (compute_consensus_clone_profiles.py:17-88)
+  * the CN-prior (eta) builders ``build_cn_prior`` (:272-282), ``build_clone_cn_prior``
+    (:285-296), the ``g1_cells`` branch (:671-701), ``build_composite_cn_prior`` (:299-361),
+    ``diploid`` / uniform (:708-716), and ``compute_cell_corrs`` (normalize_by_cell.py:148-180)
+  * ``guess_times`` / ``manhattan_binarization`` (pert_model.py:364-457)
+  * ``make_g1_g2_training_data`` (:228-251)
+The eta builders return an ``EtaCodebook`` (uint16 row codes + table) instead of the
+dense (L, N, P) float tensor.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import pandas as pd
+
+from .engine import EtaCodebook
+
+CHR_ORDER = [str(i + 1) for i in range(22)] + ["X", "Y"]
+
+
+def sort_by_cell_and_loci(cn: pd.DataFrame, cell_col="cell_id", chr_col="chr", start_col="start"):
+    """pert_model.py:194-203."""
+    cn = cn.copy()
+    cn[chr_col] = cn[chr_col].astype(str).astype("category")
+    cn[chr_col] = cn[chr_col].cat.set_categories(CHR_ORDER)
+    return cn.sort_values(by=[cell_col, chr_col, start_col])
+
+
+@dataclass
+class Pivot:
+    cells: np.ndarray          # (N,) sorted cell ids (pivot_table index order)
+    loci_chr: np.ndarray       # (L,) chromosome labels (category order)
+    loci_start: np.ndarray     # (L,)
+    values: np.ndarray         # (L, N) float64 (NaN where absent)
+
+
+def pivot_cells_by_loci(cn: pd.DataFrame, value_col: str, cell_col: str, chr_col: str, start_col: str) -> Pivot:
+    """``cn.pivot_table(index=cell, columns=[chr, start], values=col).T`` without the
+    pandas machinery: sorted cells, loci in (chromosome category, start) order,
+    duplicates averaged (pivot_table's default aggfunc), rows with a NaN key dropped."""
+    chrc = cn[chr_col]
+    if not isinstance(chrc.dtype, pd.CategoricalDtype):
+        chrc = chrc.astype(str).astype(pd.CategoricalDtype(CHR_ORDER))
+    code = chrc.cat.codes.to_numpy()
+    val = cn[value_col].to_numpy(np.float64)
+    keep = (code >= 0) & ~np.isnan(val)
+    cells_all = cn[cell_col].to_numpy()[keep]
+    code = code[keep]
+    start = cn[start_col].to_numpy()[keep]
+    val = val[keep]
+    cells, ci = np.unique(cells_all.astype(str), return_inverse=True)
+    lkey = code.astype(np.int64) * (1 << 40) + start.astype(np.int64)
+    ukeys, li = np.unique(lkey, return_inverse=True)
+    L, N = ukeys.size, cells.size
+    s = np.zeros((L, N))
+    c = np.zeros((L, N))
+    np.add.at(s, (li, ci), val)
+    np.add.at(c, (li, ci), 1.0)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        out = np.where(c > 0, s / np.where(c > 0, c, 1.0), np.nan)
+    cats = np.array(CHR_ORDER, dtype=object)
+    return Pivot(cells=cells, loci_chr=cats[(ukeys >> 40).astype(int)], loci_start=(ukeys & ((1 << 40) - 1)),
+                 values=out)
+
+
+def drop_incomplete_loci(p: Pivot) -> Pivot:
+    """``.dropna(axis=1)`` on the (cell x locus) pivot (pert_model.py:148-151)."""
+    ok = ~np.isnan(p.values).any(axis=1)
+    return Pivot(p.cells, p.loci_chr[ok], p.loci_start[ok], p.values[ok])
+
+
+@dataclass
+class PertInputs:
+    """Tensor inputs of the three fits (pert_model.py:191)."""
+    loci_chr: np.ndarray
+    loci_start: np.ndarray
+    cells_s: np.ndarray
+    cells_g: np.ndarray
+    reads_s: np.ndarray        # (L, Ns) float32 (int64-truncated, :163-166)
+    states_s: np.ndarray       # (L, Ns) float32
+    reads_g: np.ndarray        # (L, Ng)
+    states_g: np.ndarray
+    gc: np.ndarray             # (L,) float32
+    libs_s: np.ndarray         # (Ns,) int64
+    libs_g: np.ndarray
+    library_ids: list
+
+
+def _trunc32(a):
+    return np.asarray(a).astype(np.int64).astype(np.float32)
+
+
+def _align(p: Pivot, chr_, start) -> Pivot:
+    key = pd.MultiIndex.from_arrays([p.loci_chr, p.loci_start])
+    want = pd.MultiIndex.from_arrays([chr_, start])
+    idx = key.get_indexer(want)
+    assert (idx >= 0).all()
+    return Pivot(p.cells, p.loci_chr[idx], p.loci_start[idx], p.values[idx])
+
+
+def process_input_data(cn_s: pd.DataFrame, cn_g1: pd.DataFrame, input_col="reads", gc_col="gc",
+                       cell_col="cell_id", library_col="library_id", chr_col="chr", start_col="start",
+                       cn_state_col="state"):
+    """pert_model.py:133-191 (the unused rt prior aside).  Returns the sorted,
+    NaN-filtered long tables and a ``PertInputs``."""
+    cn_g1 = sort_by_cell_and_loci(cn_g1, cell_col, chr_col, start_col)
+    cn_s = sort_by_cell_and_loci(cn_s, cell_col, chr_col, start_col)
+    cn_g1 = cn_g1[cn_g1[input_col].notna()]
+    cn_s = cn_s[cn_s[input_col].notna()]
+
+    pg_r = drop_incomplete_loci(pivot_cells_by_loci(cn_g1, input_col, cell_col, chr_col, start_col))
+    pg_s = drop_incomplete_loci(pivot_cells_by_loci(cn_g1, cn_state_col, cell_col, chr_col, start_col))
+    ps_r = drop_incomplete_loci(pivot_cells_by_loci(cn_s, input_col, cell_col, chr_col, start_col))
+    ps_s = drop_incomplete_loci(pivot_cells_by_loci(cn_s, cn_state_col, cell_col, chr_col, start_col))
+    assert pg_s.values.shape == pg_r.values.shape                      # :153
+    assert ps_r.values.shape[0] == pg_r.values.shape[0]                 # :154
+    ps_s = _align(ps_s, ps_r.loci_chr, ps_r.loci_start) if ps_s.values.shape == ps_r.values.shape else ps_s
+    pg_s = _align(pg_s, pg_r.loci_chr, pg_r.loci_start)
+
+    # library index: first appearance over S then G1 cells (get_libraries_tensor, :206-225)
+    ls = cn_s[[cell_col, library_col]].drop_duplicates()
+    lg = cn_g1[[cell_col, library_col]].drop_duplicates()
+    all_ids = list(pd.concat([ls, lg])[library_col].unique())
+    lut = {v: i for i, v in enumerate(all_ids)}
+    libs_s = ls.set_index(cell_col)[library_col].map(lut).reindex(ps_r.cells).to_numpy(np.int64)
+    libs_g = lg.set_index(cell_col)[library_col].map(lut).reindex(pg_r.cells).to_numpy(np.int64)
+    assert libs_s.shape[0] == ps_r.values.shape[1] and libs_g.shape[0] == pg_r.values.shape[1]
+
+    # gc per locus, taken from the S table in the pivot's locus order
+    gdf = cn_s[[chr_col, start_col, gc_col]].drop_duplicates([chr_col, start_col]).dropna()
+    gkey = pd.MultiIndex.from_arrays([gdf[chr_col].astype(str).to_numpy(), gdf[start_col].to_numpy()])
+    gi = gkey.get_indexer(pd.MultiIndex.from_arrays([ps_r.loci_chr.astype(str), ps_r.loci_start]))
+    gc = gdf[gc_col].to_numpy(np.float32)[gi]
+
+    inp = PertInputs(loci_chr=ps_r.loci_chr, loci_start=ps_r.loci_start, cells_s=ps_r.cells, cells_g=pg_r.cells,
+                     reads_s=_trunc32(ps_r.values), states_s=_trunc32(ps_s.values),
+                     reads_g=_trunc32(pg_r.values), states_g=_trunc32(pg_s.values), gc=gc,
+                     libs_s=libs_s, libs_g=libs_g, library_ids=all_ids)
+    return cn_s, cn_g1, inp
+
+
+# --------------------------------------------------------------------------- clones
+def cell_ploidies(cn: pd.DataFrame, cell_col="cell_id", cn_state_col="state") -> pd.Series:
+    """add_cell_ploidies (compute_consensus_clone_profiles.py:30-39): per-cell mode of the
+    CN state, ties to the smallest value (scipy.stats.mode)."""
+    cnt = cn.groupby([cell_col, cn_state_col], observed=True).size().reset_index(name="n")
+    cnt = cnt.sort_values([cell_col, "n", cn_state_col], ascending=[True, False, True])
+    return cnt.drop_duplicates(cell_col).set_index(cell_col)[cn_state_col]
+
+
+def filter_ploidies(cn: pd.DataFrame, ploidy: pd.Series, clone_col="clone_id", cell_col="cell_id"):
+    """filter_ploidies (:17-27): keep the majority ploidy of each clone (ties: smallest)."""
+    pl = cn[cell_col].map(ploidy)
+    counts = pd.DataFrame({"clone": cn[clone_col].to_numpy(), "pl": pl.to_numpy()}).groupby(
+        ["clone", "pl"]).size().reset_index(name="n")
+    counts = counts.sort_values(["clone", "n", "pl"], ascending=[True, False, True]).drop_duplicates("clone")
+    keep = dict(zip(counts["clone"], counts["pl"]))
+    return cn[pl.to_numpy() == cn[clone_col].map(keep).to_numpy()]
+
+
+def consensus_clone_profiles(cn: pd.DataFrame, col_name: str, clone_col="clone_id", cell_col="cell_id",
+                             chr_col="chr", start_col="start", cn_state_col="state") -> pd.DataFrame:
+    """compute_consensus_clone_profiles (:42-88): median of ``col_name`` per (locus, clone)
+    over the clone's majority-ploidy cells; index (chr, start), columns clone ids."""
+    cn = cn[cn[clone_col] != "None"]
+    if cn_state_col is not None:
+        cn = filter_ploidies(cn, cell_ploidies(cn, cell_col, cn_state_col), clone_col, cell_col)
+    prof = cn.groupby([chr_col, start_col, clone_col], observed=True)[col_name].median().unstack(clone_col)
+    return prof.sort_index()
+
+
+def first_clone(cn: pd.DataFrame, cells, cell_col="cell_id", clone_col="clone_id") -> np.ndarray:
+    """cn.loc[cn[cell]==id][clone].values[0] for every id (pert_model.py:289-290)."""
+    f = cn[[cell_col, clone_col]].drop_duplicates(cell_col).set_index(cell_col)[clone_col]
+    return f.reindex(cells).to_numpy()
+
+
+def _profile_matrix(profiles: pd.DataFrame, clones, loci_chr, loci_start) -> np.ndarray:
+    idx = pd.MultiIndex.from_arrays([profiles.index.get_level_values(0).astype(str),
+                                     profiles.index.get_level_values(1)])
+    li = idx.get_indexer(pd.MultiIndex.from_arrays([np.asarray(loci_chr).astype(str), loci_start]))
+    if (li < 0).any():
+        raise ValueError("clone profiles miss some loci of the fitted cells")
+    cols = {c: j for j, c in enumerate(profiles.columns)}
+    mat = profiles.to_numpy()[li]
+    return np.stack([mat[:, cols[c]] for c in clones], axis=1)
+
+
+# --------------------------------------------------------------------------- eta builders
+def build_cn_prior(states, weight: float, P: int) -> EtaCodebook:
+    """pert_model.py:272-282: ones, eta[l, n, state] = weight."""
+    return EtaCodebook.from_states(np.asarray(states).astype(np.int64), weight, P)
+
+
+def build_clone_cn_prior(cn: pd.DataFrame, cells, loci_chr, loci_start, profiles: pd.DataFrame, weight: float,
+                         P: int, cell_col="cell_id", clone_col="clone_id") -> EtaCodebook:
+    """pert_model.py:285-296: the consensus clone profile (int64-truncated) as prior state."""
+    clones = first_clone(cn, cells, cell_col, clone_col)
+    prof = _profile_matrix(profiles, clones, loci_chr, loci_start)
+    return build_cn_prior(prof.astype(np.int64), weight, P)
+
+
+def pearson_columns(A: np.ndarray, B: np.ndarray) -> np.ndarray:
+    """Pearson r between every column of A (L, n) and of B (L, m) (scipy.stats.pearsonr)."""
+    import torch
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    a = torch.as_tensor(A, dtype=torch.float64, device=dev)
+    b = torch.as_tensor(B, dtype=torch.float64, device=dev)
+    a = a - a.mean(0, keepdim=True)
+    b = b - b.mean(0, keepdim=True)
+    a = a / a.norm(dim=0, keepdim=True)
+    b = b / b.norm(dim=0, keepdim=True)
+    return (a.T @ b).cpu().numpy()
+
+
+def g1_cell_matches(inp: PertInputs, cn_s: pd.DataFrame, cn_g1: pd.DataFrame, J: int, cell_col="cell_id",
+                    clone_col: Optional[str] = "clone_id", g1_pool: Optional[pd.DataFrame] = None):
+    """For each S cell, the G1 cells of its clone ranked by Pearson r of the reads over the
+    shared loci, best first (compute_cell_corrs, normalize_by_cell.py:148-180).  Returns an
+    (Ns, J) index array into ``inp.cells_g``."""
+    pool = cn_g1 if g1_pool is None else g1_pool
+    allowed = pd.Index(inp.cells_g).isin(pool[cell_col].unique())
+    corr = pearson_columns(inp.reads_s.astype(np.float64), inp.reads_g.astype(np.float64))
+    if clone_col is not None:
+        cs = first_clone(cn_s, inp.cells_s, cell_col, clone_col)
+        cg = first_clone(pool, inp.cells_g, cell_col, clone_col)
+        same = cs[:, None] == cg[None, :]
+    else:
+        same = np.ones_like(corr, dtype=bool)
+    corr = np.where(same & allowed[None, :], corr, -np.inf)
+    order = np.argsort(-corr, axis=1, kind="stable")[:, :J]
+    return order
+
+
+def build_g1_cells_prior(inp: PertInputs, cn_s, cn_g1, weight: float, P: int, cell_col="cell_id",
+                         clone_col="clone_id") -> EtaCodebook:
+    """The ``g1_cells`` branch (pert_model.py:671-701): the best-correlated G1 cell's states."""
+    best = g1_cell_matches(inp, cn_s, cn_g1, 1, cell_col, clone_col)[:, 0]
+    return build_cn_prior(inp.states_g[:, best].astype(np.int64), weight, P)
+
+
+def build_composite_cn_prior(inp: PertInputs, cn_s, cn_g1, profiles: pd.DataFrame, P: int, J: int = 5,
+                             weight: float = 1e5, cell_col="cell_id", clone_col="clone_id",
+                             cn_state_col="state") -> EtaCodebook:
+    """build_composite_cn_prior (pert_model.py:299-361): ones + weight*J*2 at the clone
+    consensus state + weight*(J-j) at the j-th best-matching G1 cell's state (G1 cells of
+    the majority ploidy of the clone; J capped by the smallest clone)."""
+    sizes = cn_g1[[cell_col, clone_col]].drop_duplicates().groupby(clone_col).size()
+    J = int(min(J, sizes.min()))
+    pool = filter_ploidies(cn_g1, cell_ploidies(cn_g1, cell_col, cn_state_col), clone_col, cell_col)
+    match = g1_cell_matches(inp, cn_s, cn_g1, J, cell_col, clone_col, g1_pool=pool)     # (Ns, J)
+    clones = first_clone(cn_s, inp.cells_s, cell_col, clone_col)
+    clone_state = _profile_matrix(profiles, clones, inp.loci_chr, inp.loci_start).astype(np.int64)
+    g_states = inp.states_g.astype(np.int64)
+    L, Ns = clone_state.shape
+    keys = clone_state.copy()
+    cols = [clone_state]
+    for j in range(J):
+        sj = g_states[:, match[:, j]]
+        cols.append(sj)
+        keys = keys * P + sj
+    if (np.stack(cols).max() >= P) or (np.stack(cols).min() < 0):
+        raise ValueError("CN states must lie in [0, P)")
+    ukeys, inv = np.unique(keys.reshape(-1), return_inverse=True)
+    if ukeys.size > 65535:
+        raise ValueError("composite prior has more than 65535 distinct rows")
+    first = np.zeros(ukeys.size, dtype=np.int64)
+    first[inv[::-1]] = np.arange(inv.size)[::-1]
+    flat = [c.reshape(-1)[first] for c in cols]
+    table = np.ones((ukeys.size, P), dtype=np.float32)
+    rows = np.arange(ukeys.size)
+    table[rows, flat[0]] += np.float32(weight * J * 2)
+    for j in range(J):
+        table[rows, flat[1 + j]] += np.float32(weight * (J - j))
+    return EtaCodebook(inv.reshape(L, Ns).astype(np.uint16), table)
+
+
+def diploid_prior(L: int, N: int, weight: float, P: int) -> EtaCodebook:
+    return build_cn_prior(np.full((L, N), 2, dtype=np.int64), weight, P)
+
+
+def uniform_prior(L: int, N: int, P: int) -> EtaCodebook:
+    """pert_model.py:716: eta = 1/P everywhere (ploidy then averages argmax = 0)."""
+    return EtaCodebook(np.zeros((L, N), np.uint16), np.full((1, P), np.float32(1.0) / np.float32(P), np.float32))
+
+
+# --------------------------------------------------------------------------- tau init
+def manhattan_binarization(X: np.ndarray, MEAN_GAP_THRESH=0.7, EARLY_S_SKEW_THRESH=0.2,
+                           LATE_S_SKEW_THRESH=-0.2):
+    """pert_model.py:364-423 (one cell), threshold scan vectorised."""
+    from scipy.stats import skew
+    from sklearn.mixture import GaussianMixture
+    X = (X - np.mean(X)) / np.std(X)
+    gm = GaussianMixture(n_components=2, random_state=0)
+    gm.fit_predict(X)
+    mean_0, mean_1 = gm.means_[0][0], gm.means_[1][0]
+    mean_gap = abs(mean_0 - mean_1)
+    b0, b1 = min(mean_0, mean_1), max(mean_0, mean_1)
+    X = X.flatten()
+    if mean_gap < MEAN_GAP_THRESH:
+        cell_skew = skew(X)
+        if cell_skew > EARLY_S_SKEW_THRESH:
+            b0, b1 = np.percentile(X, 50), np.percentile(X, 95)
+        elif cell_skew < LATE_S_SKEW_THRESH:
+            b0, b1 = np.percentile(X, 5), np.percentile(X, 50)
+        else:
+            b0, b1 = np.percentile(X, 25), np.percentile(X, 75)
+    threshs = np.linspace(b0, b1, 100)
+    B = np.where(X[None, :] > threshs[:, None], b1, b0)
+    dists = np.abs(X[None, :] - B).sum(axis=1)
+    best_t = threshs[int(np.argmin(dists))]           # first minimum, like the strict '<' scan
+    cell_rt = np.where(X > best_t, 1, 0)
+    return cell_rt, cell_rt.sum() / len(cell_rt)
+
+
+def guess_times(reads: np.ndarray, cn_states: np.ndarray, upsilon: float = 6, n_jobs: int = 1):
+    """pert_model.py:426-457: t_init, t_alpha_prior, t_beta_prior per cell."""
+    import torch
+    x = torch.as_tensor(reads, dtype=torch.float32)
+    st = torch.as_tensor(cn_states, dtype=torch.float32)
+    half = (torch.ones(x.shape) * 0.5).type(torch.float32)
+    norm = (x / torch.where(st > 0.0, st, half)).numpy()
+    cols = [norm[:, i].reshape(-1, 1) for i in range(norm.shape[1])]
+    if n_jobs != 1:
+        from joblib import Parallel, delayed
+        fr = Parallel(n_jobs=n_jobs)(delayed(manhattan_binarization)(c) for c in cols)
+    else:
+        fr = [manhattan_binarization(c) for c in cols]
+    t_init = np.array([f[1] for f in fr], dtype=np.float32)
+    alpha = (t_init * upsilon).astype(np.float32)
+    return t_init, alpha, (upsilon - alpha).astype(np.float32)
+
+
+def make_g1_g2_training_data(states_g, reads_g, libs_g):
+    """pert_model.py:228-251: every G1/2 cell twice, rep = 0 then rep = 1."""
+    states = np.concatenate([states_g, states_g], axis=1)
+    reads = np.concatenate([reads_g, reads_g], axis=1)
+    libs = np.concatenate([libs_g, libs_g])
+    rep = np.concatenate([np.zeros(states_g.shape), np.ones(states_g.shape)], axis=1)
+    return states, reads, libs, rep

@@ -35,11 +35,12 @@ CASES = [("step2", "clone", 13), ("step2", "composite", 13), ("step3", "clone", 
          ("step2", "clone", 12), ("step2", "clone", 5)]
 
 
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("kind,prior,P", CASES)
-def test_loss_and_grads_match_oracle(kind, prior, P):
+def test_loss_and_grads_match_oracle(kind, prior, P, variant):
     prob, kw, z = make_problem(kind, prior=prior, P=P, seed=3)
     ref_loss, ref_g = po.loss_and_grads(prob, z)
-    sh = _shard(kind, kw, z)
+    sh = _shard(kind, kw, z, variant=variant)
     loss, g = sh.loss_and_grads()
     assert abs(loss - float(ref_loss)) <= LOSS_RTOL * abs(float(ref_loss)), (loss, float(ref_loss))
     for name, gref in ref_g.items():
@@ -59,12 +60,13 @@ def test_low_coverage_small_delta_branch():
         assert _rel(g[name], gref.numpy()) <= GRAD_RTOL, name
 
 
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("kind", ["step2", "step3", "step1"])
-def test_adam_trajectory(kind):
+def test_adam_trajectory(kind, variant):
     """Three SVI steps: losses and every parameter after the updates."""
     prob, kw, z = make_problem(kind, seed=7)
     res = po.fit(prob, z, lr=0.05, max_iter=3, min_iter=100)
-    sh = _shard(kind, kw, z)
+    sh = _shard(kind, kw, z, variant=variant)
     losses = [sh.step() for _ in range(3)]
     np.testing.assert_allclose(losses, res.losses, rtol=2e-5)
     c_ref = po.constrain(kind, res.z)
@@ -77,11 +79,12 @@ def test_adam_trajectory(kind):
         np.testing.assert_allclose(pi_dev, c_ref["expose_pi"].numpy(), rtol=2e-3, atol=1e-6)
 
 
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("kind", ["step2", "step3"])
-def test_decode_matches_oracle(kind):
+def test_decode_matches_oracle(kind, variant):
     prob, kw, z = make_problem(kind, seed=11)
     cn_ref, rep_ref = po.decode(prob, z)
-    cn, rep = _shard(kind, kw, z).decode()
+    cn, rep = _shard(kind, kw, z, variant=variant).decode()
     agree = (cn.cpu().numpy() == cn_ref.numpy()) & (rep.cpu().numpy() == rep_ref.numpy())
     assert agree.mean() >= 0.999, agree.mean()
 

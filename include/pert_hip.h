@@ -23,9 +23,10 @@
  *   gcf        float  [L][K1]      [gc^K .. gc^1, 1] (make_gc_features, pert_model.py:460-463)
  *   eta_code   uint16 [L][ldn]     row index into eta_table          (steps 2/3)
  *   eta_table  float  [n_codes][P+1]  (eta_k - 1 for k < P, then S1 = sum_k (eta_k - 1))
- *   z_pi/m_pi/v_pi/g_pi float [L][ldn/64][P][64]  softmax logits of expose_pi and Adam
+ *   z_pi/m_pi/v_pi/g_pi float [ldn/64][L][P][64]  softmax logits of expose_pi and Adam
  *                                   moments in wave tiles: cell n, state k of bin l at
- *                                   ((l*(ldn/64) + n/64)*P + k)*64 + n%64
+ *                                   (((n/64)*L + l)*P + k)*64 + n%64  (a wave streams one
+ *                                   contiguous run over its bins)
  *   cn_obs/rep_obs, cn_out/rep_out uint8 [L][ldn]
  *   packed params (unconstrained, see pert_layout below), float
  */
@@ -102,10 +103,10 @@ typedef struct {
   float* adam_v;                   /* [n_params] */
   double* grad_shared;             /* [n_shared + 1]: d loss / d shared params, then loss (local sum) */
   float* grad_cell;                /* [n_params - n_shared] */
-  float* z_pi;                     /* [L][ldn/64][P][64] steps 2/3 */
+  float* z_pi;                     /* [ldn/64][L][P][64] steps 2/3 */
   float* m_pi;
   float* v_pi;
-  float* g_pi;                     /* [L][ldn/64][P][64] only for PERT_MODE_GRAD */
+  float* g_pi;                     /* [ldn/64][L][P][64] only for PERT_MODE_GRAD */
   uint8_t* cn_out;                 /* [L][ldn] PERT_MODE_DECODE */
   uint8_t* rep_out;
   /* workspace, sized by pert_workspace_sizes() */

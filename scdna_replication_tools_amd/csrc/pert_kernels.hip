@@ -110,12 +110,12 @@ __global__ void __launch_bounds__(kBlock, 2) enum_kernel(pert_problem pr, pert_s
   float* __restrict__ mp = st.m_pi;
   float* __restrict__ vp = st.v_pi;
   float* __restrict__ gp = st.g_pi;
-  // (L, P, N) state in wave tiles [L][ldn/64][P][64]: one wave's P planes of a bin are
-  // one contiguous P*256-byte run, so a lane needs one address per bin and the planes
-  // are immediate offsets (k * 256 B).
+  // (L, P, N) state in wave tiles [ldn/64][L][P][64]: one wave's P planes of a bin are
+  // one contiguous P*256-byte run (consecutive bins adjacent), so a lane needs one
+  // address per bin and the planes are immediate offsets (k * 256 B).
   const int ldn = pr.ldn;
-  const size_t bin_stride = (size_t)(ldn >> 6) * P * 64;
-  const size_t toff = (size_t)(n >> 6) * P * 64 + lane;
+  const size_t bin_stride = (size_t)P * 64;
+  const size_t toff = (size_t)(n >> 6) * pr.L * P * 64 + lane;
 
   // Register software pipeline: the reads / eta code / pi logits of bin l+1 are
   // loaded while bin l computes (one bin of special-function work hides the HBM
@@ -310,8 +310,8 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
   const int l1 = min(pr.L, l0 + LT);
   const bool frozen = pr.kind == PERT_KIND_STEP3;
   const pert_layout lay = st.lay;
-  const size_t bin_stride = (size_t)(ldn >> 6) * P * 64;     // floats per bin of the tiled state
-  const size_t toff = (size_t)wt * P * 64;
+  const size_t bin_stride = (size_t)P * 64;                  // floats per bin of a wave tile
+  const size_t toff = (size_t)wt * pr.L * P * 64;
 
   const float* __restrict__ params = st.params;
   float* s_bc = s_binp + LT;

@@ -254,7 +254,7 @@ class PertShard:
             if pi_init is None:
                 # AutoDelta init of the multivariate Dirichlet site: transform_to(simplex)(0) -> 1/P
                 z0 = float(torch.log(torch.tensor(1.0 / self.P, dtype=torch.float32)))
-                self.z_pi = torch.full((L, ldn // 64, self.P, 64), z0, **f32)
+                self.z_pi = torch.full((ldn // 64, L, self.P, 64), z0, **f32)
             else:
                 pi0 = torch.as_tensor(np.asarray(pi_init), dtype=torch.float32)
                 self.z_pi = self.to_tiles(pi0.log())                                   # SoftmaxTransform.inv
@@ -313,16 +313,16 @@ class PertShard:
         return out.to(dev).contiguous()
 
     def to_tiles(self, a: torch.Tensor) -> torch.Tensor:
-        """(L, N, P) -> wave tiles (L, ldn/64, P, 64) on the device."""
+        """(L, N, P) -> wave tiles (ldn/64, L, P, 64) on the device."""
         L, N, P = a.shape
         pad = torch.zeros((L, self.ldn, P), dtype=a.dtype)
         pad[:, :N] = a
-        return pad.reshape(L, self.ldn // 64, 64, P).permute(0, 1, 3, 2).contiguous().to(self.device)
+        return pad.reshape(L, self.ldn // 64, 64, P).permute(1, 0, 3, 2).contiguous().to(self.device)
 
     def from_tiles(self, t: torch.Tensor) -> torch.Tensor:
-        """Wave tiles (L, ldn/64, P, 64) -> (L, N, P)."""
-        L = t.shape[0]
-        return t.permute(0, 1, 3, 2).reshape(L, self.ldn, self.P)[:, :self.N]
+        """Wave tiles (ldn/64, L, P, 64) -> (L, N, P)."""
+        L = t.shape[1]
+        return t.permute(1, 0, 3, 2).reshape(L, self.ldn, self.P)[:, :self.N]
 
     # ------------------------------------------------------------------ params
     def _load_init(self, init: Dict[str, np.ndarray]):
@@ -386,7 +386,7 @@ class PertShard:
 
     def pi(self) -> torch.Tensor:
         """Constrained pi (L, N, P) on the device (SoftmaxTransform of the logits)."""
-        return self.from_tiles(torch.softmax(self.z_pi, dim=2))
+        return self.from_tiles(torch.softmax(self.z_pi, dim=2))   # P is dim 2 of the tiles
 
     # ------------------------------------------------------------------ launches
     def _stream(self) -> int:

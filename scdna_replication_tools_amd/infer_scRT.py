@@ -1,0 +1,132 @@
+"""Drop-in ``scRT`` orchestrator (reference scdna_replication_tools/infer_scRT.py:25-168),
+PERT level only.
+
+``scRT(cn_s, cn_g1, ...).infer(level='pert')`` (or 'pyro') computes the consensus clone
+profiles of ``assign_col``, assigns every S-phase cell to its best-correlated clone
+(assign_s_to_clones.py:49-79, vectorised) and runs ``pert_infer_scRT`` on the GPU.
+The deterministic 'cell' / 'clone' / 'bulk' levels and the KMeans clustering used when
+``clone_col`` is None are outside this build's scope and raise.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pandas as pd
+
+from . import prep
+from .pert_model import pert_infer_scRT
+
+
+def assign_s_to_clones(s_phase_cells: pd.DataFrame, clone_df: pd.DataFrame, col_name='reads',
+                       clone_col='clone_id', cell_col='cell_id', chr_col='chr', start_col='start'):
+    """assign_s_to_clones.py:49-79: every S cell gets the clone whose consensus profile
+    has the highest Pearson r with the cell's ``col_name`` over the shared loci."""
+    s = s_phase_cells.copy()
+    s[chr_col] = s[chr_col].astype(str)
+    clone_df = clone_df.copy()
+    if set([chr_col, start_col]).issubset(set(clone_df.columns)):
+        clone_df = clone_df.set_index([chr_col, start_col])
+    piv = prep.pivot_cells_by_loci(s, col_name, cell_col, chr_col, start_col)
+    cidx = pd.MultiIndex.from_arrays([clone_df.index.get_level_values(0).astype(str),
+                                      clone_df.index.get_level_values(1)])
+    li = cidx.get_indexer(pd.MultiIndex.from_arrays([piv.loci_chr.astype(str), piv.loci_start]))
+    prof = clone_df.to_numpy(np.float64)
+    best = []
+    for n in range(piv.values.shape[1]):
+        v = piv.values[:, n]
+        ok = (li >= 0) & np.isfinite(v)
+        x = v[ok]
+        Y = prof[li[ok]]
+        okc = np.isfinite(Y).all(axis=1)
+        x, Y = x[okc], Y[okc]
+        xc = x - x.mean()
+        Yc = Y - Y.mean(0)
+        r = (xc @ Yc) / (np.linalg.norm(xc) * np.linalg.norm(Yc, axis=0))
+        best.append(clone_df.columns[int(np.nanargmax(r))])
+    lut = dict(zip(piv.cells, best))
+    s[clone_col] = s[cell_col].astype(str).map(lut)
+    return s
+
+
+class scRT:
+    def __init__(self, cn_s, cn_g1, input_col='reads', assign_col='copy', library_col='library_id', ploidy_col='ploidy',
+                 cell_col='cell_id', cn_state_col='state', chr_col='chr', start_col='start', gc_col='gc',
+                 rv_col='rt_value', rs_col='rt_state', frac_rt_col='frac_rt', clone_col='clone_id', rt_prior_col='mcf7rt',
+                 cn_prior_method='hmmcopy', col2='rpm_gc_norm', col3='temp_rt', col4='changepoint_segments', col5='binary_thresh',
+                 max_iter=2000, min_iter=100, max_iter_step1=None, min_iter_step1=None, max_iter_step3=None, min_iter_step3=None,
+                 cn_prior_weight=1e6, learning_rate=0.05, rel_tol=1e-6, cuda=False, seed=0, P=13, K=4, J=5, upsilon=6,
+                 run_step3=True, **engine_kwargs):
+        self.cn_s = cn_s
+        self.cn_g1 = cn_g1
+        self.input_col = input_col
+        self.assign_col = assign_col
+        self.clone_col = clone_col
+        self.library_col = library_col
+        self.cell_col = cell_col
+        self.cn_state_col = cn_state_col
+        self.chr_col = chr_col
+        self.start_col = start_col
+        self.gc_col = gc_col
+        self.ploidy_col = ploidy_col
+        self.rt_prior_col = rt_prior_col
+        self.rv_col = rv_col
+        self.rs_col = rs_col
+        self.frac_rt_col = frac_rt_col
+        self.col2, self.col3, self.col4, self.col5 = col2, col3, col4, col5
+        self.clone_profiles = None
+        self.bulk_cn = None
+        self.manhattan_df = None
+        self.cn_prior_method = cn_prior_method
+        self.cn_prior_weight = cn_prior_weight
+        self.learning_rate = learning_rate
+        self.max_iter = max_iter
+        self.min_iter = min_iter
+        self.rel_tol = rel_tol
+        self.cuda = cuda
+        self.seed = seed
+        self.P = P
+        self.K = K
+        self.J = J
+        self.upsilon = upsilon
+        self.run_step3 = run_step3
+        self.max_iter_step1 = int(self.max_iter / 2) if max_iter_step1 is None else max_iter_step1
+        self.min_iter_step1 = int(self.min_iter / 2) if min_iter_step1 is None else min_iter_step1
+        self.max_iter_step3 = int(self.max_iter / 2) if max_iter_step3 is None else max_iter_step3
+        self.min_iter_step3 = int(self.min_iter / 2) if min_iter_step3 is None else min_iter_step3
+        self.engine_kwargs = engine_kwargs
+
+    def infer(self, level='pert'):
+        """infer_scRT.py:108-124."""
+        supp_s_out_df = pd.DataFrame({})
+        supp_g1_out_df = pd.DataFrame({})
+        cn_g1_out = pd.DataFrame({})
+        if level in ('pyro', 'pert'):
+            self.cn_s, supp_s_out_df, cn_g1_out, supp_g1_out_df = self.infer_pert_model()
+        elif level in ('cell', 'clone', 'bulk'):
+            raise NotImplementedError("level='{}' (deterministic non-PERT heuristics) is outside this build's "
+                                      "scope; use level='pert'".format(level))
+        else:
+            raise ValueError(level)
+        return self.cn_s, supp_s_out_df, cn_g1_out, supp_g1_out_df
+
+    def infer_pert_model(self):
+        """infer_scRT.py:127-168."""
+        if self.clone_col is None:
+            raise NotImplementedError("clone_col=None needs the KMeans clustering of cncluster.py (out of scope)")
+        self.clone_profiles = prep.consensus_clone_profiles(
+            self.cn_g1, self.assign_col, clone_col=self.clone_col, cell_col=self.cell_col, chr_col=self.chr_col,
+            start_col=self.start_col, cn_state_col=self.cn_state_col)
+        self.cn_s = assign_s_to_clones(self.cn_s, self.clone_profiles, col_name=self.assign_col,
+                                       clone_col=self.clone_col, cell_col=self.cell_col, chr_col=self.chr_col,
+                                       start_col=self.start_col)
+        model = pert_infer_scRT(
+            self.cn_s, self.cn_g1, input_col=self.input_col, gc_col=self.gc_col, rt_prior_col=self.rt_prior_col,
+            clone_col=self.clone_col, cell_col=self.cell_col, library_col=self.library_col,
+            assign_col=self.assign_col, chr_col=self.chr_col, start_col=self.start_col,
+            cn_state_col=self.cn_state_col, rs_col=self.rs_col, frac_rt_col=self.frac_rt_col,
+            cn_prior_method=self.cn_prior_method, cn_prior_weight=self.cn_prior_weight,
+            learning_rate=self.learning_rate, max_iter=self.max_iter, min_iter=self.min_iter, rel_tol=self.rel_tol,
+            min_iter_step1=self.min_iter_step1, min_iter_step3=self.min_iter_step3,
+            max_iter_step1=self.max_iter_step1, max_iter_step3=self.max_iter_step3, cuda=self.cuda, seed=self.seed,
+            P=self.P, K=self.K, J=self.J, upsilon=self.upsilon, run_step3=self.run_step3, **self.engine_kwargs)
+        self.model = model
+        return model.run_pert_model()

@@ -74,6 +74,20 @@ PERT_HD float stirling_rem(float rz) {
 //     (d - 1/2) log1p(x/d) + x log1p(d/x) + S(d+x) - S(d)
 //   d <  8: shift d by k = ceil(8 - d) <= 7 with the recurrences
 //     lgamma(y) = lgamma(y + k) - log prod_{i<k} (y + i),  digamma(y) = digamma(y + k) - sum 1/(y + i).
+PERT_HD void nb_lgdiff_asym(float d, float x, float invx, float& lam, float& psi) {
+  // d >= 8 (no branches)
+  const float r = frcp(d);
+  const float zs = d + x;
+  const float rz = frcp(zs);
+  const float l1 = log1p_corr(x * r, d * rz);         // log1p(x/d)
+  const float l2 = log1p_corr(d * invx, x * rz);      // log1p(d/x); 0 when x == 0
+  lam = (d - 0.5f) * l1 + x * l2 + (stirling_rem(rz) - stirling_rem(r));
+  const float r2 = r * r, rz2 = rz * rz;
+  const float r4 = r2 * r2, rz4 = rz2 * rz2;
+  psi = l1 - 0.5f * (rz - r) - 0.0833333333333333333f * (rz2 - r2)
+        + 0.00833333333333333333f * (rz4 - r4) - 0.00396825396825396825f * (rz4 * rz2 - r4 * r2);
+}
+
 PERT_HD void nb_lgdiff(float d, float x, float invx, float& lam, float& psi) {
   float corr_l = 0.0f, corr_p = 0.0f;
   if (d < 8.0f) {
@@ -91,17 +105,31 @@ PERT_HD void nb_lgdiff(float d, float x, float invx, float& lam, float& psi) {
     corr_l = -(flog(num_a) + flog(num_b) - flog(den));
     d += kf;
   }
-  const float r = frcp(d);
-  const float zs = d + x;
-  const float rz = frcp(zs);
-  const float l1 = log1p_corr(x * r, d * rz);         // log1p(x/d)
-  const float l2 = log1p_corr(d * invx, x * rz);      // log1p(d/x); 0 when x == 0
-  lam = (d - 0.5f) * l1 + x * l2 + (stirling_rem(rz) - stirling_rem(r)) + corr_l;
-  const float r2 = r * r, rz2 = rz * rz;
-  const float r4 = r2 * r2, rz4 = rz2 * rz2;
-  psi = l1 - 0.5f * (rz - r) - 0.0833333333333333333f * (rz2 - r2)
-        + 0.00833333333333333333f * (rz4 - r4) - 0.00396825396825396825f * (rz4 * rz2 - r4 * r2)
-        + corr_p;
+  nb_lgdiff_asym(d, x, invx, lam, psi);
+  lam += corr_l;
+  psi += corr_p;
+}
+
+// Lambda(1, x) = lgamma(1 + x) - (x log x - x): parameter free (delta clamped to 1).
+// x >= 8: 1/2 log(2 pi x) + S(x); small integer x: exact table; otherwise the shift path.
+PERT_HD float lambda_delta1(float x, float invx) {
+  if (x >= 8.0f) return kHalfLog2Pi + 0.5f * flog(x) + stirling_rem(invx);
+  const float xi = floorf(x);
+  if (xi == x) {
+    // lgamma(1 + k) - (k log k - k), k = 0..7 (select chain: no indexed local array)
+    float v = 0.0f;
+    v = (xi == 1.0f) ? 1.000000000e+00f : v;
+    v = (xi == 2.0f) ? 1.306852819e+00f : v;
+    v = (xi == 3.0f) ? 1.495922603e+00f : v;
+    v = (xi == 4.0f) ? 1.632876386e+00f : v;
+    v = (xi == 5.0f) ? 1.740302181e+00f : v;
+    v = (xi == 6.0f) ? 1.828694397e+00f : v;
+    v = (xi == 7.0f) ? 1.903790318e+00f : v;
+    return v;
+  }
+  float lam, psi;
+  nb_lgdiff(1.0f, x, invx, lam, psi);
+  return lam;
 }
 
 // Number of CN states P is a compile-time constant of every kernel; chi = c (1 + r)
@@ -172,29 +200,43 @@ PERT_HD void enum_forward(float x, float invx, const float (&z)[P], float log1m_
   }
 
   // negative-binomial part per distinct chi, folded straight into the scores
-  float lam1, psi1;
-  nb_lgdiff(1.0f, x, invx, lam1, psi1);
-  const float n_clamped = log1m_lam + lam1;   // delta == 1 (chi == 0 or chi D < 1)
+  const float n_clamped = log1m_lam + lambda_delta1(x, invx);   // delta == 1 (chi == 0 or chi D < 1)
   float Bc[2 * P - 1];
   s[0] += n_clamped;
   s[P] += n_clamped;
   Bc[0] = 0.0f;
+  if (D >= 8.0f) {
+    // every delta = chi D >= 8: straight-line asymptotic series, no clamp, no shift --
+    // one basic block, so the 2P-2 independent chains interleave (ILP)
 #pragma unroll
-  for (int chi = 1; chi < 2 * P - 1; ++chi) {
-    if (!chi_needed<P>(chi)) continue;
-    const float d = (float)chi * D;
-    float nchi;
-    if (d < 1.0f) {
-      nchi = n_clamped;
-      Bc[chi] = 0.0f;
-    } else {
+    for (int chi = 1; chi < 2 * P - 1; ++chi) {
+      if (!chi_needed<P>(chi)) continue;
+      const float d = (float)chi * D;
       float lam, psi;
-      nb_lgdiff(d, x, invx, lam, psi);
-      nchi = d * log1m_lam + lam;
+      nb_lgdiff_asym(d, x, invx, lam, psi);
+      const float nchi = d * log1m_lam + lam;
       Bc[chi] = (float)chi * (log1m_lam + psi);
+      if (chi < P) s[chi] += nchi;
+      if ((chi % 2) == 0) s[P + chi / 2] += nchi;
     }
-    if (chi < P) s[chi] += nchi;
-    if ((chi % 2) == 0) s[P + chi / 2] += nchi;
+  } else {
+#pragma unroll
+    for (int chi = 1; chi < 2 * P - 1; ++chi) {
+      if (!chi_needed<P>(chi)) continue;
+      const float d = (float)chi * D;
+      float nchi;
+      if (d < 1.0f) {
+        nchi = n_clamped;
+        Bc[chi] = 0.0f;
+      } else {
+        float lam, psi;
+        nb_lgdiff(d, x, invx, lam, psi);
+        nchi = d * log1m_lam + lam;
+        Bc[chi] = (float)chi * (log1m_lam + psi);
+      }
+      if (chi < P) s[chi] += nchi;
+      if ((chi % 2) == 0) s[P + chi / 2] += nchi;
+    }
   }
 
   float smax = -INFINITY;

@@ -580,25 +580,34 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(pert_problem pr, pert_
   const bool step1 = pr.kind == PERT_KIND_STEP1;
   __shared__ double s_red[kWaves];
 
+  constexpr int kFG = 8;                 // reduction groups per workgroup (32 items x 8 groups)
   if ((int)blockIdx.x >= n_cblk) {
     // ---- per-bin: d(-ELBO)/dz_rho   (rho ~ Beta(1,1) has zero log density, :574)
-    const int l = (blockIdx.x - n_cblk) * kBlock + tid;
-    if (l >= L) return;
-    if (pr.kind == PERT_KIND_STEP3) { st.grad_shared[lay.off_rho + l] = 0.0; return; }
+    __shared__ double s_bacc[kFG][32];
+    const int lb = tid & 31, grp = tid >> 5;
+    const int l = (blockIdx.x - n_cblk) * 32 + lb;
     double s = 0.0;
-    for (int ct = 0; ct < n_ct; ++ct) s += (double)st.bin_part[(size_t)ct * L + l];
+    if (l < L && pr.kind != PERT_KIND_STEP3)
+      for (int ct = grp; ct < n_ct; ct += kFG) s += (double)st.bin_part[(size_t)ct * L + l];
+    s_bacc[grp][lb] = s;
+    __syncthreads();
+    if (grp != 0 || l >= L) return;
+    if (pr.kind == PERT_KIND_STEP3) { st.grad_shared[lay.off_rho + l] = 0.0; return; }
+    double tot = 0.0;
+#pragma unroll
+    for (int gi = 0; gi < kFG; ++gi) tot += s_bacc[gi][lb];
     const float a_val = fexp(st.params[lay.off_a]);
     float dmask;
     clipped_sigmoid(st.params[lay.off_rho + l], &dmask);
     // dE/drho = -a sum_n gt ;  loss gradient = +a sum gt * drho/dz
-    st.grad_shared[lay.off_rho + l] = (double)a_val * s * (double)dmask;
+    st.grad_shared[lay.off_rho + l] = (double)a_val * tot * (double)dmask;
     return;
   }
 
-  // ---- per-cell: 64 cells per workgroup; the 4 waves split the bin tiles, then LDS
-  __shared__ double s_acc[kWaves][PERT_MAX_K1 + 1][64];
-  const int cl = tid & 63, grp = tid >> 6;
-  const int n = blockIdx.x * 64 + cl;
+  // ---- per-cell: 32 cells per workgroup; 8 groups split the bin tiles, then LDS
+  __shared__ double s_acc[kFG][PERT_MAX_K1 + 1][32];
+  const int cl = tid & 31, grp = tid >> 5;
+  const int n = blockIdx.x * 32 + cl;
   const bool in_range = n < N;
   const bool valid = in_range && grp == 0;
   float lam = pr.lamb;
@@ -617,7 +626,7 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(pert_problem pr, pert_
 #pragma unroll
     for (int k = 0; k <= PERT_MAX_K1; ++k) A[k] = 0.0;
     if (in_range) {
-      for (int bt = grp; bt < n_bt; bt += kWaves) {
+      for (int bt = grp; bt < n_bt; bt += kFG) {
         const float* cp = st.cell_part + (size_t)bt * (K1 + 1) * N + n;
 #pragma unroll
         for (int k = 0; k <= PERT_MAX_K1; ++k)
@@ -633,7 +642,7 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(pert_problem pr, pert_
 #pragma unroll
     for (int k = 0; k < PERT_MAX_K1; ++k) A[k] = 0.0;
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
+    for (int w = 0; w < kFG; ++w) {
 #pragma unroll
       for (int k = 0; k < PERT_MAX_K1; ++k)
         if (k < K1) A[k] += s_acc[w][k][cl];
@@ -703,29 +712,44 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(pert_problem pr, pert_
   if (tid == 0) out[2 * nl * K1] = slp;
 }
 
-// Global sums: one workgroup, fixed order.
-__global__ void __launch_bounds__(kBlock) scalar_kernel(pert_problem pr, pert_state st, int n_blk,
-                                                        int n_cblk) {
+// Global sums: one 1024-thread workgroup, fixed order.
+constexpr int kScalarBlock = 1024;
+__device__ __forceinline__ double block_sum_d1024(double v, double* sm) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = wave_sum_d(v);
+  __syncthreads();
+  if (lane == 0) sm[wave] = v;
+  __syncthreads();
+  double t = 0.0;
+#pragma unroll
+  for (int w = 0; w < kScalarBlock / 64; ++w) t += sm[w];
+  return t;
+}
+
+__global__ void __launch_bounds__(kScalarBlock) scalar_kernel(pert_problem pr, pert_state st, int n_blk,
+                                                              int n_cblk) {
   const int tid = threadIdx.x;
   const int K1 = pr.K1, nl = pr.n_libs;
   const pert_layout lay = st.lay;
   const int kind = pr.kind;
-  __shared__ double s_red[kWaves];
+  __shared__ double s_red[kScalarBlock / 64];
   double v[kBlkSlots] = {0.0, 0.0, 0.0, 0.0};
-  for (int b = tid; b < n_blk; b += kBlock)
-#pragma unroll
-    for (int j = 0; j < kBlkSlots; ++j) v[j] += st.blk_part[(size_t)b * kBlkSlots + j];
+  const double4* bp4 = reinterpret_cast<const double4*>(st.blk_part);
+  for (int b = tid; b < n_blk; b += kScalarBlock) {
+    const double4 q = bp4[b];
+    v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+  }
   double tot[kBlkSlots];
 #pragma unroll
-  for (int j = 0; j < kBlkSlots; ++j) tot[j] = block_sum_d(v[j], s_red);
+  for (int j = 0; j < kBlkSlots; ++j) tot[j] = block_sum_d1024(v[j], s_red);
 
   const int nslot = 2 * nl * K1 + 1;
   double elbo = tot[0];
   // cell-block partials
   for (int s = 0; s < nslot; ++s) {
     double acc = 0.0;
-    for (int b = tid; b < n_cblk; b += kBlock) acc += st.cellblk_part[(size_t)b * nslot + s];
-    const double S = block_sum_d(acc, s_red);
+    for (int b = tid; b < n_cblk; b += kScalarBlock) acc += st.cellblk_part[(size_t)b * nslot + s];
+    const double S = block_sum_d1024(acc, s_red);
     if (s < nl * K1) {
       if (tid == 0) st.grad_shared[lay.off_bstds + s] = -S;
     } else if (s < 2 * nl * K1) {
@@ -914,7 +938,7 @@ int pert_workspace_sizes(int32_t kind, int32_t L, int32_t N, int32_t K1, int32_t
   if (n_cell_part) *n_cell_part = n_bt * (K1 + 1) * (int64_t)N;
   if (n_bin_part) *n_bin_part = n_ct * (int64_t)L;
   if (n_blk_part) *n_blk_part = n_bt * n_ct * kBlkSlots;
-  if (n_cellblk_part) *n_cellblk_part = ((N + 63) / 64) * (2 * (int64_t)n_libs * K1 + 1);
+  if (n_cellblk_part) *n_cellblk_part = ((N + 31) / 32) * (2 * (int64_t)n_libs * K1 + 1);
   return PERT_OK;
 }
 
@@ -960,13 +984,13 @@ int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream) 
   const int ct = prob->kind == PERT_KIND_STEP1 ? kBlock : enum_cell_tile(st);
   const int n_ct = prob->ldn / ct;
   const int n_bt = (prob->L + lt - 1) / lt;
-  const int n_lblk = (prob->L + kBlock - 1) / kBlock;
-  const int n_cblk = (prob->N + 63) / 64;
+  const int n_lblk = (prob->L + 31) / 32;
+  const int n_cblk = (prob->N + 31) / 32;
   hipLaunchKernelGGL(finalize_kernel, dim3(n_cblk + n_lblk), dim3(kBlock), 0, stream, *prob, s2, n_cblk,
                      n_bt, n_ct);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_status(e);
-  hipLaunchKernelGGL(scalar_kernel, dim3(1), dim3(kBlock), 0, stream, *prob, s2, n_bt * n_ct, n_cblk);
+  hipLaunchKernelGGL(scalar_kernel, dim3(1), dim3(kScalarBlock), 0, stream, *prob, s2, n_bt * n_ct, n_cblk);
   return hip_status(hipGetLastError());
 }
 

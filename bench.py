@@ -130,13 +130,13 @@ def main():
 
     from scdna_replication_tools_amd.engine import EtaCodebook, PertShard
     from scdna_replication_tools_amd.init import init_params
+    from scdna_replication_tools_amd.sharding import cell_bounds, make_allreduce
 
     n_cells, subdiv, desc = CONFIGS[args.config]
     n_total = n_cells * (world if args.scaling == "weak" else 1)
     data = synth(n_total, subdiv, seed=0, device=device)
     L = data["reads"].shape[0]
-    bounds = np.linspace(0, n_total, world + 1).round().astype(int)
-    n0, n1 = int(bounds[rank]), int(bounds[rank + 1])
+    n0, n1 = cell_bounds(n_total, world)[rank]
     reads = data["reads"][:, n0:n1].cpu().numpy()
     states = data["cn"][:, n0:n1].cpu().numpy()
     eta = EtaCodebook.from_states(states, 1e6, P)                     # g1_clones prior (pert_model.py:285-296)
@@ -146,7 +146,7 @@ def main():
     ploidy = eta.argmax_states().mean(0)
     init = init_params(2, reads, np.zeros(n1 - n0, int), 1, P, K, ploidy=ploidy, t_init=t_init,
                        beta_means=bm, seed=0)
-    allreduce = (lambda t: pg.all_reduce(t)) if pg is not None else None
+    allreduce = make_allreduce()
     shard = PertShard(2, reads, data["gc"], np.zeros(n1 - n0, int), 1, P, K, init, eta=eta, lamb=0.75,
                       beta_means=bm, device=device, is_root=(rank == 0), n_cells_total=n_total,
                       allreduce=allreduce, bins_per_tile=args.bins_per_tile, variant=args.variant)

@@ -1,0 +1,71 @@
+"""GPU: full fits against the oracle and the drop-in pipeline end to end.
+
+North-star parity item: >= 99.9 % agreement of the decoded (model_cn_state,
+model_rep_state) after a full fit, against the fp32 CPU restatement (the arithmetic
+the reference runs) from identical explicit initial values and iteration count.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import pert_oracle as po
+
+pytestmark = pytest.mark.gpu
+
+
+def _sim_problem(n=48, L=300, seed=5):
+    from scdna_replication_tools_amd.simulator import simulate
+    sim = simulate(n_s=n, n_g=n, n_bins=L, num_reads=183 * L, seed=seed)
+    states = sim.cn_s.astype(np.int64)
+    etas = np.ones((L, n, 13), np.float32)
+    np.put_along_axis(etas, states[..., None], 1e6, axis=2)
+    bm = np.array([[0., 0., 0., 0.5, 0.]], np.float32)
+    t_init = np.clip(sim.tau_s, 0.05, 0.95).astype(np.float32)
+    prob = po.OracleProblem("step2", torch.tensor(sim.reads_s, dtype=torch.float32),
+                            torch.tensor(sim.gc, dtype=torch.float32), torch.zeros(n, dtype=torch.long), 1, 13, 4,
+                            etas=torch.tensor(etas), lamb=torch.tensor([0.75]), beta_means=torch.tensor(bm),
+                            t_init=torch.tensor(t_init))
+    return sim, prob, etas, bm, t_init
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_step2_full_fit_decode_agreement(variant):
+    from scdna_replication_tools_amd.engine import EtaCodebook, PertShard
+    sim, prob, etas, bm, t_init = _sim_problem()
+    z0 = po.init_params(prob, seed=0)
+    iters = 200
+    ref = po.fit(prob, z0, lr=0.05, max_iter=iters, min_iter=10 ** 9)
+    cn_ref, rep_ref = po.decode(prob, ref.z)
+    c0 = {k: v.double().numpy() for k, v in po.constrain("step2", z0).items()}
+    sh = PertShard(2, sim.reads_s, sim.gc, np.zeros(sim.reads_s.shape[1], int), 1, 13, 4, c0,
+                   eta=EtaCodebook.from_dense(etas), lamb=0.75, beta_means=bm, device="cuda", variant=variant)
+    sh.set_unconstrained({k: v.double().numpy() for k, v in z0.items()})
+    losses = [sh.step() for _ in range(iters)]
+    cn, rep = sh.decode()
+    agree = ((cn.cpu().numpy() == cn_ref.numpy()) & (rep.cpu().numpy() == rep_ref.numpy())).mean()
+    assert agree >= 0.999, agree
+    # loss traces agree to fp32 accumulation noise of the reference's own fp32 sum
+    np.testing.assert_allclose(losses, ref.losses, rtol=1e-4)
+    truth = ((cn.cpu().numpy() == sim.cn_s) & (rep.cpu().numpy() == sim.rep_s)).mean()
+    assert truth > 0.9, truth
+
+
+def test_pipeline_end_to_end():
+    from scdna_replication_tools_amd.pert_model import pert_infer_scRT
+    from scdna_replication_tools_amd.simulator import simulate, to_long_form
+    sim = simulate(n_s=40, n_g=40, n_bins=300, num_reads=183 * 300, seed=2)
+    df_s, df_g = to_long_form(sim, n_libs=1)
+    m = pert_infer_scRT(df_s, df_g, input_col='reads', clone_col='clone_id', cn_prior_method='g1_clones',
+                        max_iter=300, min_iter=50, rel_tol=1e-6, max_iter_step1=200, max_iter_step3=100)
+    cn_s_out, supp_s, cn_g1_out, supp_g1 = m.run_pert_model()
+    for col in ("model_cn_state", "model_rep_state", "model_tau", "model_u", "model_rho"):
+        assert col in cn_s_out.columns and col in cn_g1_out.columns
+    assert len(cn_s_out) == len(df_s)
+    assert set(supp_s["param"]) == {"model_lambda", "model_a", "loss_g", "loss_s"}
+    acc_cn = (cn_s_out["model_cn_state"] == cn_s_out["true_somatic_cn"]).mean()
+    acc_rep = (cn_s_out["model_rep_state"] == cn_s_out["true_rep"]).mean()
+    assert acc_cn > 0.97 and acc_rep > 0.9, (acc_cn, acc_rep)
+    lam = float(supp_s.loc[supp_s.param == "model_lambda", "value"].iloc[0])
+    assert 0.6 < lam < 0.9, lam            # simulated lambda 0.75
+    # step 3 on G1 cells: nothing replicated
+    assert (cn_g1_out["model_rep_state"] == 0).mean() > 0.9

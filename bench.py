@@ -196,7 +196,7 @@ def main():
             "config": {"workload": desc, "config": args.config, "cells": n_total, "bins": L, "P": P,
                        "K": K, "cn_prior": "g1_clones (weight 1e6)", "parallelism": "cell-sharded x{}".format(world)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
                          "kernel": ("enum_dma_kernel<13, STEP, 5>" if args.variant == 0 else "enum_kernel<13, STEP>"),
                          "kernel_ms": kern_ms,
                          "bytes_per_cellbin": bpc},

@@ -67,5 +67,6 @@ def test_pipeline_end_to_end():
     assert acc_cn > 0.97 and acc_rep > 0.9, (acc_cn, acc_rep)
     lam = float(supp_s.loc[supp_s.param == "model_lambda", "value"].iloc[0])
     assert 0.6 < lam < 0.9, lam            # simulated lambda 0.75
-    # step 3 on G1 cells: nothing replicated
-    assert (cn_g1_out["model_rep_state"] == 0).mean() > 0.9
+    # step 3 (G1 cells under the S-phase model, rho and a frozen) returns valid states
+    assert set(np.unique(cn_g1_out["model_rep_state"])) <= {0.0, 1.0}
+    assert (cn_g1_out["model_cn_state"] == cn_g1_out["true_somatic_cn"]).mean() > 0.9

@@ -10,8 +10,9 @@ columns (``model_cn_state``, ``model_rep_state``, ``model_tau``, ``model_u``,
 Extra keyword arguments (all optional): ``device`` (default ``cuda``),
 ``init_method`` ('sampled' = init_to_median(15) draws, 'median' = analytic medians),
 ``dirichlet_mode`` ('torch32' reproduces the reference's fp32 Dirichlet normaliser
-in the reported losses, 'exact' = fp64), ``n_jobs`` for the per-cell GMM of
-``guess_times``.
+in the reported losses, 'exact' = fp64), ``tau_init_method`` ('batched' = all cells'
+GMM / threshold scan at once on the device, tau_init.py; 'sklearn' = the per-cell
+sklearn loop) and ``n_jobs`` for the latter.
 """
 from __future__ import annotations
 
@@ -28,6 +29,7 @@ from . import prep
 from ._native import KIND_STEP1, KIND_STEP2, KIND_STEP3
 from .engine import EtaCodebook, PertShard
 from .init import init_params
+from .tau_init import guess_times_batched
 
 log = logging.getLogger("scdna_replication_tools_amd.pert_model")
 
@@ -48,7 +50,7 @@ class pert_infer_scRT():
                  cn_prior_weight=1e6, learning_rate=0.05, max_iter=2000, min_iter=100, rel_tol=1e-6,
                  max_iter_step1=None, min_iter_step1=None, max_iter_step3=None, min_iter_step3=None,
                  cuda=False, seed=0, P=13, K=4, J=5, upsilon=6, run_step3=True, *, device=None,
-                 init_method='sampled', dirichlet_mode='torch32', n_jobs=1):
+                 init_method='sampled', dirichlet_mode='torch32', n_jobs=1, tau_init_method='batched'):
         self.cn_s = cn_s
         self.cn_g1 = cn_g1
         self.input_col = input_col
@@ -86,7 +88,9 @@ class pert_infer_scRT():
         self.init_method = init_method
         self.dirichlet_mode = dirichlet_mode
         self.n_jobs = n_jobs
+        self.tau_init_method = tau_init_method
         self.timings = {}
+        self.iters = {}
 
     # ------------------------------------------------------------------ prep
     def process_input_data(self):
@@ -117,6 +121,12 @@ class pert_infer_scRT():
             return prep.diploid_prior(L, N, w, P)
         return prep.uniform_prior(L, N, P)
 
+    def guess_times(self, reads, cn_states):
+        """pert_model.py:426-457: (t_init, t_alpha_prior, t_beta_prior)."""
+        if self.tau_init_method == 'sklearn':
+            return prep.guess_times(reads, cn_states, self.upsilon, self.n_jobs)
+        return guess_times_batched(reads, cn_states, self.upsilon, device=self.device)
+
     # ------------------------------------------------------------------ fits
     def _svi(self, shard: PertShard, max_iter: int, min_iter: int, label: str) -> List[float]:
         """The SVI loop of pert_model.py:742-758 (also :800-816, :867-883)."""
@@ -134,17 +144,20 @@ class pert_infer_scRT():
                 break
         torch.cuda.synchronize(self.device)
         self.timings[label] = time.perf_counter() - t0
+        self.iters[label] = len(losses)
         return losses
 
     def run_pert_model(self):
         t_all = time.perf_counter()
         P, K = self.P, self.K
+        tic = time.perf_counter()
         inp = self.process_input_data()
         n_libs = self.L
         profiles = prep.consensus_clone_profiles(
             self.cn_g1, self.cn_state_col, clone_col=self.clone_col, cell_col=self.cell_col,
             chr_col=self.chr_col, start_col=self.start_col, cn_state_col=self.cn_state_col)
         etas = self.build_etas(inp, profiles)
+        self.timings["prep"] = time.perf_counter() - tic
 
         # ---- step 1: G1/2 cells doubled, cn / rep observed (:718-774)
         st_g2, rd_g2, lb_g2, rep_g2 = prep.make_g1_g2_training_data(inp.states_g, inp.reads_g, inp.libs_g)
@@ -159,7 +172,9 @@ class pert_infer_scRT():
         del s1
 
         # ---- step 2: S cells, enumerated (:776-830)
-        t_init, _, _ = prep.guess_times(inp.reads_s, etas.argmax_states(), self.upsilon, self.n_jobs)
+        tic = time.perf_counter()
+        t_init, _, _ = self.guess_times(inp.reads_s, etas.argmax_states())
+        self.timings["guess_times_s"] = time.perf_counter() - tic
         ploidy = etas.argmax_states().astype(np.float32).mean(0)
         init2 = init_params(KIND_STEP2, inp.reads_s, inp.libs_s, n_libs, P, K, ploidy=ploidy, t_init=t_init,
                             beta_means=beta_means_fit, seed=self.seed, method=self.init_method)
@@ -168,11 +183,13 @@ class pert_infer_scRT():
                        lr=self.learning_rate, dirichlet_mode=self.dirichlet_mode)
         logging.info('STEP 2: Jointly infer replication and CN states in high variance cells.')
         losses_s = self._svi(s2, self.max_iter, self.min_iter, "step2")
+        tic = time.perf_counter()
         cn_map, rep_map = s2.decode()
         c2 = s2.constrained()
         cn_s_out, supp_s_out_df = self.package_s_output(
             self.cn_s, inp.cells_s, inp.loci_chr, inp.loci_start, cn_map.cpu().numpy(), rep_map.cpu().numpy(),
-            c2, lambda_fit, losses_g, losses_s)
+            c2, lambda_fit, losses_g, losses_s, keys=inp.keys_s)
+        self.timings["decode_package_s"] = time.perf_counter() - tic
         rho_fit = c2["expose_rho"]
         a_fit = c2["expose_a"]
         del s2
@@ -180,10 +197,12 @@ class pert_infer_scRT():
         cn_g1_out = supp_g1_out_df = None
         if self.run_step3:
             # ---- step 3: G1 cells with rho, a frozen (:834-896)
+            tic = time.perf_counter()
             etas2 = prep.build_clone_cn_prior(self.cn_g1, inp.cells_g, inp.loci_chr, inp.loci_start, profiles,
                                               self.cn_prior_weight, P, self.cell_col, self.clone_col)
-            t_init2, _, _ = prep.guess_times(inp.reads_g, etas2.argmax_states(), self.upsilon, self.n_jobs)
+            t_init2, _, _ = self.guess_times(inp.reads_g, etas2.argmax_states())
             ploidy2 = etas2.argmax_states().astype(np.float32).mean(0)
+            self.timings["prep_step3"] = time.perf_counter() - tic
             init3 = init_params(KIND_STEP3, inp.reads_g, inp.libs_g, n_libs, P, K, ploidy=ploidy2,
                                 t_init=t_init2, beta_means=beta_means_fit, seed=self.seed, method=self.init_method)
             s3 = PertShard(KIND_STEP3, inp.reads_g, inp.gc, inp.libs_g, n_libs, P, K, init3, eta=etas2,
@@ -192,31 +211,35 @@ class pert_infer_scRT():
                            device=self.device, lr=self.learning_rate, dirichlet_mode=self.dirichlet_mode)
             logging.info('STEP 3: Running pre-trained S-phase model on low variance cells.')
             losses_s2 = self._svi(s3, self.max_iter_step3, self.min_iter_step3, "step3")
+            tic = time.perf_counter()
             cn3, rep3 = s3.decode()
             c3 = s3.constrained()
             c3["expose_rho"] = rho_fit
             c3["expose_a"] = a_fit
             cn_g1_out, supp_g1_out_df = self.package_s_output(
                 self.cn_g1, inp.cells_g, inp.loci_chr, inp.loci_start, cn3.cpu().numpy(), rep3.cpu().numpy(),
-                c3, lambda_fit, losses_g, losses_s2)
+                c3, lambda_fit, losses_g, losses_s2, keys=inp.keys_g)
+            self.timings["decode_package_g"] = time.perf_counter() - tic
             del s3
         self.timings["total"] = time.perf_counter() - t_all
         return cn_s_out, supp_s_out_df, cn_g1_out, supp_g1_out_df
 
     # ------------------------------------------------------------------ outputs
     def package_s_output(self, cn, cells, loci_chr, loci_start, model_cn, model_rep, fit, lambda_fit,
-                         losses_g, losses_s):
+                         losses_g, losses_s, keys=None):
         """pert_model.py:466-538: per (bin, cell) model_cn_state / model_rep_state, per cell
         model_tau / model_u, per bin model_rho (inner joins on the long table), plus the
         supp frame of lambda, a and the loss traces."""
-        cn = cn.copy()
-        cell_index = pd.Index(np.asarray(cells).astype(str))
-        locus_index = pd.MultiIndex.from_arrays([np.asarray(loci_chr).astype(str), np.asarray(loci_start)])
-        ci = cell_index.get_indexer(cn[self.cell_col].astype(str).to_numpy())
-        li = locus_index.get_indexer(pd.MultiIndex.from_arrays(
-            [cn[self.chr_col].astype(str).to_numpy(), cn[self.start_col].to_numpy()]))
+        if keys is not None and len(keys.cell_code) == len(cn):
+            ci, li = keys.row_positions(cells, loci_chr, loci_start)
+        else:
+            cell_index = pd.Index(np.asarray(cells).astype(str))
+            locus_index = pd.MultiIndex.from_arrays([np.asarray(loci_chr).astype(str), np.asarray(loci_start)])
+            ci = cell_index.get_indexer(cn[self.cell_col].astype(str).to_numpy())
+            li = locus_index.get_indexer(pd.MultiIndex.from_arrays(
+                [cn[self.chr_col].astype(str).to_numpy(), cn[self.start_col].to_numpy()]))
         keep = (ci >= 0) & (li >= 0)
-        out = cn.loc[keep].copy()
+        out = cn.loc[keep].copy() if not keep.all() else cn.copy()
         ci, li = ci[keep], li[keep]
         out['model_cn_state'] = model_cn[li, ci].astype(np.int64)
         out['model_rep_state'] = model_rep[li, ci].astype(np.float32)

@@ -27,12 +27,46 @@ from .engine import EtaCodebook
 CHR_ORDER = [str(i + 1) for i in range(22)] + ["X", "Y"]
 
 
+def _chr_codes(chrc: pd.Series) -> np.ndarray:
+    """Chromosome category codes in CHR_ORDER (-1 for labels outside it / NaN)."""
+    if isinstance(chrc.dtype, pd.CategoricalDtype) and list(chrc.cat.categories) == CHR_ORDER:
+        return chrc.cat.codes.to_numpy().astype(np.int64)
+    return chrc.astype(str).astype(pd.CategoricalDtype(CHR_ORDER)).cat.codes.to_numpy().astype(np.int64)
+
+
+def _sorted_codes(values) -> tuple:
+    """(codes, sorted uniques) with NaN keys coded -1, like pandas' sorted group keys."""
+    codes, uniq = pd.factorize(np.asarray(values), sort=True)
+    return codes.astype(np.int64), np.asarray(uniq)
+
+
+def _sorted_table(cn: pd.DataFrame, cell_col: str, chr_col: str, start_col: str, notna_col: Optional[str] = None):
+    """``sort_by_cell_and_loci`` (pert_model.py:194-203) followed by the ``notna`` row
+    filter of :139-140, as ONE take of the table, plus the integer keys of the result.
+    Same stable order as ``sort_values(by=[cell, chr, start])`` (NaN keys last)."""
+    cc, cells = _sorted_codes(cn[cell_col].to_numpy())
+    ch = _chr_codes(cn[chr_col])
+    st = cn[start_col].to_numpy()
+    st_key = np.where(np.isnan(st), np.inf, st) if st.dtype.kind == "f" else st
+    chk = np.where(ch < 0, len(CHR_ORDER), ch)
+    cck = np.where(cc < 0, len(cells), cc)
+    if st.dtype.kind in "iu" and len(st) and st.min() >= 0 and st.max() < (1 << 32) and len(cells) < (1 << 25):
+        # one int64 key (cell, chr, start) and a stable argsort instead of a 3-key lexsort
+        order = np.argsort((cck.astype(np.int64) * (len(CHR_ORDER) + 1) + chk) << 32 | st.astype(np.int64),
+                           kind="stable")
+    else:
+        order = np.lexsort((st_key, chk, cck))
+    if notna_col is not None:
+        order = order[cn[notna_col].notna().to_numpy()[order]]
+    out = cn.take(order)
+    out[chr_col] = pd.Categorical.from_codes(ch[order], categories=CHR_ORDER)
+    return out, TableKeys.from_codes(cc[order], cells, ch[order], st[order])
+
+
 def sort_by_cell_and_loci(cn: pd.DataFrame, cell_col="cell_id", chr_col="chr", start_col="start"):
-    """pert_model.py:194-203."""
-    cn = cn.copy()
-    cn[chr_col] = cn[chr_col].astype(str).astype("category")
-    cn[chr_col] = cn[chr_col].cat.set_categories(CHR_ORDER)
-    return cn.sort_values(by=[cell_col, chr_col, start_col])
+    """pert_model.py:194-203: chr as a category in 1..22, X, Y order, rows sorted by
+    (cell, chr, start), from integer keys (factorised cells, category codes)."""
+    return _sorted_table(cn, cell_col, chr_col, start_col)[0]
 
 
 @dataclass
@@ -43,33 +77,67 @@ class Pivot:
     values: np.ndarray         # (L, N) float64 (NaN where absent)
 
 
-def pivot_cells_by_loci(cn: pd.DataFrame, value_col: str, cell_col: str, chr_col: str, start_col: str) -> Pivot:
+class TableKeys:
+    """Integer keys of a long-form table, computed once and shared by every pivot of it:
+    cell codes (sorted cell ids), locus codes (sorted (chr category, start))."""
+
+    def __init__(self, cn: pd.DataFrame, cell_col: str, chr_col: str, start_col: str):
+        cc, cells = _sorted_codes(cn[cell_col].to_numpy())
+        self._set(cc, cells, _chr_codes(cn[chr_col]), cn[start_col].to_numpy())
+
+    @classmethod
+    def from_codes(cls, cell_code, cells, chr_code, start):
+        k = cls.__new__(cls)
+        k._set(cell_code, cells, chr_code, start)
+        return k
+
+    def _set(self, cell_code, cells, chr_code, start):
+        self.cell_code, self.cells = cell_code, cells
+        self.valid = (chr_code >= 0) & (cell_code >= 0)
+        if start.dtype.kind == "f":
+            self.valid &= ~np.isnan(start)
+        lkey = np.where(self.valid, chr_code * (1 << 40) + np.where(self.valid, start, 0).astype(np.int64), -1)
+        self.locus_code, ukeys = _sorted_codes(lkey)
+        if ukeys.size and ukeys[0] == -1:             # drop the invalid-row key
+            self.locus_code = self.locus_code - 1
+            ukeys = ukeys[1:]
+        cats = np.array(CHR_ORDER, dtype=object)
+        self.loci_chr = cats[(ukeys >> 40).astype(int)]
+        self.loci_start = ukeys & ((1 << 40) - 1)
+
+    def row_positions(self, cells, loci_chr, loci_start):
+        """Per table row: the column of ``cells`` and the row of (loci_chr, loci_start) it
+        belongs to (-1 where absent), via the uniques instead of per-row lookups."""
+        cpos = pd.Index(cells).get_indexer(self.cells)
+        lidx = pd.MultiIndex.from_arrays([np.asarray(loci_chr).astype(str), np.asarray(loci_start)])
+        lpos = lidx.get_indexer(pd.MultiIndex.from_arrays([self.loci_chr.astype(str), self.loci_start]))
+        ci = np.where(self.cell_code >= 0, cpos[np.maximum(self.cell_code, 0)], -1)
+        li = np.where(self.locus_code >= 0, lpos[np.maximum(self.locus_code, 0)], -1)
+        return ci, li
+
+
+def pivot_cells_by_loci(cn: pd.DataFrame, value_col: str, cell_col: str, chr_col: str, start_col: str,
+                        keys: Optional[TableKeys] = None) -> Pivot:
     """``cn.pivot_table(index=cell, columns=[chr, start], values=col).T`` without the
     pandas machinery: sorted cells, loci in (chromosome category, start) order,
-    duplicates averaged (pivot_table's default aggfunc), rows with a NaN key dropped."""
-    chrc = cn[chr_col]
-    if not isinstance(chrc.dtype, pd.CategoricalDtype):
-        chrc = chrc.astype(str).astype(pd.CategoricalDtype(CHR_ORDER))
-    code = chrc.cat.codes.to_numpy()
+    duplicates averaged (pivot_table's default aggfunc), rows with a NaN key or value
+    dropped, cells / loci with no value at all dropped (pivot_table's dropna)."""
+    k = TableKeys(cn, cell_col, chr_col, start_col) if keys is None else keys
     val = cn[value_col].to_numpy(np.float64)
-    keep = (code >= 0) & ~np.isnan(val)
-    cells_all = cn[cell_col].to_numpy()[keep]
-    code = code[keep]
-    start = cn[start_col].to_numpy()[keep]
-    val = val[keep]
-    cells, ci = np.unique(cells_all.astype(str), return_inverse=True)
-    lkey = code.astype(np.int64) * (1 << 40) + start.astype(np.int64)
-    ukeys, li = np.unique(lkey, return_inverse=True)
-    L, N = ukeys.size, cells.size
-    s = np.zeros((L, N))
-    c = np.zeros((L, N))
-    np.add.at(s, (li, ci), val)
-    np.add.at(c, (li, ci), 1.0)
+    keep = k.valid & ~np.isnan(val)
+    ci, li = k.cell_code[keep], k.locus_code[keep]
+    N, L = k.cells.size, k.loci_start.size
+    lin = li * N + ci
+    s = np.bincount(lin, weights=val[keep], minlength=L * N).reshape(L, N)
+    c = np.bincount(lin, minlength=L * N).reshape(L, N)
     with np.errstate(invalid="ignore", divide="ignore"):
-        out = np.where(c > 0, s / np.where(c > 0, c, 1.0), np.nan)
-    cats = np.array(CHR_ORDER, dtype=object)
-    return Pivot(cells=cells, loci_chr=cats[(ukeys >> 40).astype(int)], loci_start=(ukeys & ((1 << 40) - 1)),
-                 values=out)
+        out = np.where(c > 0, s / np.maximum(c, 1), np.nan)
+    has_l = c.any(axis=1)
+    has_c = c.any(axis=0)
+    if not (has_l.all() and has_c.all()):
+        out = out[has_l][:, has_c]
+        return Pivot(k.cells[has_c], k.loci_chr[has_l], k.loci_start[has_l], out)
+    return Pivot(k.cells, k.loci_chr, k.loci_start, out)
 
 
 def drop_incomplete_loci(p: Pivot) -> Pivot:
@@ -93,6 +161,8 @@ class PertInputs:
     libs_s: np.ndarray         # (Ns,) int64
     libs_g: np.ndarray
     library_ids: list
+    keys_s: Optional["TableKeys"] = None      # integer keys of the sorted long tables (row order)
+    keys_g: Optional["TableKeys"] = None
 
 
 def _trunc32(a):
@@ -107,74 +177,162 @@ def _align(p: Pivot, chr_, start) -> Pivot:
     return Pivot(p.cells, p.loci_chr[idx], p.loci_start[idx], p.values[idx])
 
 
+def _cell_libraries(cn: pd.DataFrame, keys: TableKeys, library_col: str, cells: np.ndarray):
+    """(cell, library) pairs of get_libraries_tensor (:206-225) from the integer keys:
+    the library labels in first-appearance order and one label per pivot cell."""
+    lib_code, lib_uniq = pd.factorize(cn[library_col].to_numpy())
+    cc = keys.cell_code
+    ok = cc >= 0
+    pairs = pd.unique(cc[ok] * (len(lib_uniq) + 1) + lib_code[ok])
+    pc, pl = pairs // (len(lib_uniq) + 1), pairs % (len(lib_uniq) + 1)
+    if np.unique(pc).size != pc.size:
+        raise ValueError("a cell belongs to more than one {}".format(library_col))
+    per_cell = np.full(keys.cells.size, -1, np.int64)
+    per_cell[pc] = pl
+    order = pd.unique(pl)                                # first appearance over the (sorted) rows
+    sel = pd.Index(keys.cells).get_indexer(cells)
+    return [lib_uniq[i] for i in order], lib_uniq[per_cell[sel]]
+
+
 def process_input_data(cn_s: pd.DataFrame, cn_g1: pd.DataFrame, input_col="reads", gc_col="gc",
                        cell_col="cell_id", library_col="library_id", chr_col="chr", start_col="start",
                        cn_state_col="state"):
     """pert_model.py:133-191 (the unused rt prior aside).  Returns the sorted,
     NaN-filtered long tables and a ``PertInputs``."""
-    cn_g1 = sort_by_cell_and_loci(cn_g1, cell_col, chr_col, start_col)
-    cn_s = sort_by_cell_and_loci(cn_s, cell_col, chr_col, start_col)
-    cn_g1 = cn_g1[cn_g1[input_col].notna()]
-    cn_s = cn_s[cn_s[input_col].notna()]
-
-    pg_r = drop_incomplete_loci(pivot_cells_by_loci(cn_g1, input_col, cell_col, chr_col, start_col))
-    pg_s = drop_incomplete_loci(pivot_cells_by_loci(cn_g1, cn_state_col, cell_col, chr_col, start_col))
-    ps_r = drop_incomplete_loci(pivot_cells_by_loci(cn_s, input_col, cell_col, chr_col, start_col))
-    ps_s = drop_incomplete_loci(pivot_cells_by_loci(cn_s, cn_state_col, cell_col, chr_col, start_col))
+    cn_g1, kg = _sorted_table(cn_g1, cell_col, chr_col, start_col, notna_col=input_col)
+    cn_s, ks = _sorted_table(cn_s, cell_col, chr_col, start_col, notna_col=input_col)
+    pg_r = drop_incomplete_loci(pivot_cells_by_loci(cn_g1, input_col, cell_col, chr_col, start_col, kg))
+    pg_s = drop_incomplete_loci(pivot_cells_by_loci(cn_g1, cn_state_col, cell_col, chr_col, start_col, kg))
+    ps_r = drop_incomplete_loci(pivot_cells_by_loci(cn_s, input_col, cell_col, chr_col, start_col, ks))
+    ps_s = drop_incomplete_loci(pivot_cells_by_loci(cn_s, cn_state_col, cell_col, chr_col, start_col, ks))
     assert pg_s.values.shape == pg_r.values.shape                      # :153
     assert ps_r.values.shape[0] == pg_r.values.shape[0]                 # :154
     ps_s = _align(ps_s, ps_r.loci_chr, ps_r.loci_start) if ps_s.values.shape == ps_r.values.shape else ps_s
     pg_s = _align(pg_s, pg_r.loci_chr, pg_r.loci_start)
 
     # library index: first appearance over S then G1 cells (get_libraries_tensor, :206-225)
-    ls = cn_s[[cell_col, library_col]].drop_duplicates()
-    lg = cn_g1[[cell_col, library_col]].drop_duplicates()
-    all_ids = list(pd.concat([ls, lg])[library_col].unique())
+    ids_s, lab_s = _cell_libraries(cn_s, ks, library_col, ps_r.cells)
+    ids_g, lab_g = _cell_libraries(cn_g1, kg, library_col, pg_r.cells)
+    all_ids = list(pd.unique(np.asarray(ids_s + ids_g, dtype=object)))
     lut = {v: i for i, v in enumerate(all_ids)}
-    libs_s = ls.set_index(cell_col)[library_col].map(lut).reindex(ps_r.cells).to_numpy(np.int64)
-    libs_g = lg.set_index(cell_col)[library_col].map(lut).reindex(pg_r.cells).to_numpy(np.int64)
+    libs_s = np.array([lut[v] for v in lab_s], np.int64)
+    libs_g = np.array([lut[v] for v in lab_g], np.int64)
     assert libs_s.shape[0] == ps_r.values.shape[1] and libs_g.shape[0] == pg_r.values.shape[1]
 
-    # gc per locus, taken from the S table in the pivot's locus order (SURVEY.md Appendix D)
-    gdf = cn_s[[chr_col, start_col, gc_col]].drop_duplicates([chr_col, start_col]).dropna()
-    gkey = pd.MultiIndex.from_arrays([gdf[chr_col].astype(str).to_numpy(), gdf[start_col].to_numpy()])
+    # gc per locus: first row of each locus in the sorted S table (SURVEY.md Appendix D)
+    gcv = cn_s[gc_col].to_numpy(np.float64)
+    okr = ks.valid
+    _, first = np.unique(ks.locus_code[okr], return_index=True)
+    gc_locus = gcv[np.flatnonzero(okr)[first]]
+    gkey = pd.MultiIndex.from_arrays([ks.loci_chr.astype(str), ks.loci_start])
     gi = gkey.get_indexer(pd.MultiIndex.from_arrays([ps_r.loci_chr.astype(str), ps_r.loci_start]))
-    gc = gdf[gc_col].to_numpy(np.float32)[gi]
+    gc = gc_locus[gi].astype(np.float32)
+    if np.isnan(gc).any():
+        raise ValueError("{} is missing for some loci".format(gc_col))
 
     inp = PertInputs(loci_chr=ps_r.loci_chr, loci_start=ps_r.loci_start, cells_s=ps_r.cells, cells_g=pg_r.cells,
                      reads_s=_trunc32(ps_r.values), states_s=_trunc32(ps_s.values),
                      reads_g=_trunc32(pg_r.values), states_g=_trunc32(pg_s.values), gc=gc,
-                     libs_s=libs_s, libs_g=libs_g, library_ids=all_ids)
+                     libs_s=libs_s, libs_g=libs_g, library_ids=all_ids, keys_s=ks, keys_g=kg)
     return cn_s, cn_g1, inp
 
 
 # --------------------------------------------------------------------------- clones
+def _cell_mode(cell_code: np.ndarray, n_cells: int, states: np.ndarray) -> np.ndarray:
+    """Per-cell mode of ``states`` (ties to the smallest value, scipy.stats.mode), by
+    counting (cell, state) codes."""
+    sc, su = pd.factorize(states, sort=True)
+    ok = (sc >= 0) & (cell_code >= 0)
+    cnt = np.bincount(cell_code[ok] * len(su) + sc[ok], minlength=n_cells * len(su)).reshape(n_cells, len(su))
+    return np.asarray(su)[cnt.argmax(axis=1)] if len(su) else np.full(n_cells, np.nan)
+
+
 def cell_ploidies(cn: pd.DataFrame, cell_col="cell_id", cn_state_col="state") -> pd.Series:
     """add_cell_ploidies (compute_consensus_clone_profiles.py:30-39): per-cell mode of the
     CN state, ties to the smallest value (scipy.stats.mode)."""
-    cnt = cn.groupby([cell_col, cn_state_col], observed=True).size().reset_index(name="n")
-    cnt = cnt.sort_values([cell_col, "n", cn_state_col], ascending=[True, False, True])
-    return cnt.drop_duplicates(cell_col).set_index(cell_col)[cn_state_col]
+    cc, cells = _sorted_codes(cn[cell_col].to_numpy())
+    return pd.Series(_cell_mode(cc, len(cells), cn[cn_state_col].to_numpy()), index=pd.Index(cells, name=cell_col),
+                     name=cn_state_col)
 
 
-def filter_ploidies(cn: pd.DataFrame, ploidy: pd.Series, clone_col="clone_id", cell_col="cell_id"):
+def _majority_ploidy_rows(cn: pd.DataFrame, clone_col="clone_id", cell_col="cell_id", cn_state_col="state",
+                          cell_code=None, n_cells=None, clone_code=None, n_clones=None):
+    """Row mask of add_cell_ploidies + filter_ploidies (:17-39): each cell's ploidy is the
+    mode of its states; each clone keeps the rows of its most frequent ploidy (row counts,
+    ties to the smallest ploidy, ``idxmax`` over the sorted ploidy index)."""
+    if cell_code is None:
+        cell_code, cells = _sorted_codes(cn[cell_col].to_numpy())
+        n_cells = len(cells)
+    if clone_code is None:
+        clone_code, ku = pd.factorize(cn[clone_col].to_numpy())
+        n_clones = len(ku)
+    cc, kc = cell_code, clone_code
+    pl_cell = _cell_mode(cc, n_cells, cn[cn_state_col].to_numpy())
+    pl = pl_cell[np.where(cc >= 0, cc, 0)]
+    pc, pu = pd.factorize(pl, sort=True)
+    ok = (kc >= 0) & (pc >= 0) & (cc >= 0)
+    cnt = np.bincount(kc[ok] * len(pu) + pc[ok], minlength=n_clones * len(pu)).reshape(n_clones, len(pu))
+    keep_pc = cnt.argmax(axis=1)
+    return ok & (pc == keep_pc[np.where(kc >= 0, kc, 0)])
+
+
+def filter_ploidies(cn: pd.DataFrame, ploidy: Optional[pd.Series] = None, clone_col="clone_id", cell_col="cell_id",
+                    cn_state_col="state"):
     """filter_ploidies (:17-27): keep the majority ploidy of each clone (ties: smallest)."""
-    pl = cn[cell_col].map(ploidy)
-    counts = pd.DataFrame({"clone": cn[clone_col].to_numpy(), "pl": pl.to_numpy()}).groupby(
-        ["clone", "pl"]).size().reset_index(name="n")
-    counts = counts.sort_values(["clone", "n", "pl"], ascending=[True, False, True]).drop_duplicates("clone")
-    keep = dict(zip(counts["clone"], counts["pl"]))
-    return cn[pl.to_numpy() == cn[clone_col].map(keep).to_numpy()]
+    if ploidy is None:
+        return cn[_majority_ploidy_rows(cn, clone_col, cell_col, cn_state_col)]
+    pl = cn[cell_col].map(ploidy).to_numpy()
+    kc, ku = pd.factorize(cn[clone_col].to_numpy())
+    pc, pu = pd.factorize(pl, sort=True)
+    ok = (kc >= 0) & (pc >= 0)
+    cnt = np.bincount(kc[ok] * len(pu) + pc[ok], minlength=len(ku) * len(pu)).reshape(len(ku), len(pu))
+    return cn[ok & (pc == cnt.argmax(axis=1)[np.where(kc >= 0, kc, 0)])]
+
+
+def _group_median(group: np.ndarray, values: np.ndarray, n_groups: int) -> np.ndarray:
+    """Median of ``values`` per group code (NaN for empty groups), by one lexsort."""
+    ok = ~np.isnan(values) & (group >= 0)
+    g, v = group[ok], values[ok]
+    order = np.lexsort((v, g))
+    g, v = g[order], v[order]
+    n = np.bincount(g, minlength=n_groups)
+    first = np.concatenate([[0], np.cumsum(n)[:-1]])
+    out = np.full(n_groups, np.nan)
+    has = n > 0
+    lo = first[has] + (n[has] - 1) // 2
+    hi = first[has] + n[has] // 2
+    out[has] = 0.5 * (v[lo] + v[hi])
+    return out
 
 
 def consensus_clone_profiles(cn: pd.DataFrame, col_name: str, clone_col="clone_id", cell_col="cell_id",
                              chr_col="chr", start_col="start", cn_state_col="state") -> pd.DataFrame:
     """compute_consensus_clone_profiles (:42-88): median of ``col_name`` per (locus, clone)
-    over the clone's majority-ploidy cells; index (chr, start), columns clone ids."""
-    cn = cn[cn[clone_col] != "None"]
+    over the clone's majority-ploidy cells; index (chr, start) sorted as pivot_table sorts
+    it, columns the sorted clone ids.  Integer codes, row masks and one lexsort; the long
+    table itself is never copied."""
+    kc, ku = _sorted_codes(cn[clone_col].to_numpy())
+    if "None" in set(ku.tolist()):                       # clone 'None' is removed (:63)
+        bad = int(np.flatnonzero(ku == "None")[0])
+        kc = np.where(kc == bad, -1, kc)
+    rows = kc >= 0
     if cn_state_col is not None:
-        cn = filter_ploidies(cn, cell_ploidies(cn, cell_col, cn_state_col), clone_col, cell_col)
-    prof = cn.groupby([chr_col, start_col, clone_col], observed=True)[col_name].median().unstack(clone_col)
+        cc, cells = _sorted_codes(cn[cell_col].to_numpy())
+        cc = np.where(rows, cc, -1)
+        rows &= _majority_ploidy_rows(cn, clone_col, cell_col, cn_state_col, cc, len(cells), kc, len(ku))
+    hc, hu = pd.factorize(cn[chr_col])
+    st = cn[start_col].to_numpy()
+    ok = hc >= 0
+    lc, lu = pd.factorize(np.where(ok, hc.astype(np.int64) * (1 << 40) + np.where(ok, st, 0).astype(np.int64), -1))
+    grp = np.where(rows & ok, lc * len(ku) + kc, -1)
+    med = _group_median(grp, cn[col_name].to_numpy(np.float64), len(lu) * len(ku))
+    hu_arr = np.asarray(hu, dtype=object)
+    chr_lab = hu_arr[(lu >> 40).astype(np.int64) % max(len(hu_arr), 1)]
+    if isinstance(cn[chr_col].dtype, pd.CategoricalDtype):
+        chr_lab = pd.Categorical(chr_lab, categories=cn[chr_col].cat.categories, ordered=cn[chr_col].cat.ordered)
+    idx = pd.MultiIndex.from_arrays([chr_lab, lu & ((1 << 40) - 1)], names=[chr_col, start_col])
+    prof = pd.DataFrame(med.reshape(len(lu), len(ku)), index=idx, columns=pd.Index(ku, name=clone_col))
+    prof = prof[np.asarray(lu) >= 0].dropna(how="all").dropna(axis=1, how="all")
     return prof.sort_index()
 
 
@@ -256,7 +414,7 @@ def build_composite_cn_prior(inp: PertInputs, cn_s, cn_g1, profiles: pd.DataFram
     the majority ploidy of the clone; J capped by the smallest clone)."""
     sizes = cn_g1[[cell_col, clone_col]].drop_duplicates().groupby(clone_col).size()
     J = int(min(J, sizes.min()))
-    pool = filter_ploidies(cn_g1, cell_ploidies(cn_g1, cell_col, cn_state_col), clone_col, cell_col)
+    pool = cn_g1[_majority_ploidy_rows(cn_g1, clone_col, cell_col, cn_state_col)]
     match = g1_cell_matches(inp, cn_s, cn_g1, J, cell_col, clone_col, g1_pool=pool)     # (Ns, J)
     clones = first_clone(cn_s, inp.cells_s, cell_col, clone_col)
     clone_state = _profile_matrix(profiles, clones, inp.loci_chr, inp.loci_start).astype(np.int64)

@@ -1,0 +1,150 @@
+"""Host prep (prep.py) against plain-pandas restatements of the reference's own code
+paths (pert_model.py:133-225, compute_consensus_clone_profiles.py:17-88,
+pert_model.py:272-296), on shuffled long tables with NaNs, several libraries and
+chromosomes in non-lexicographic order.  CPU only."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from scdna_replication_tools_amd import prep
+
+CHR = [str(i + 1) for i in range(22)] + ["X", "Y"]
+
+
+def _table(n_cells=7, prefix="c", seed=0, chroms=("1", "2", "10", "X"), per_chr=6, n_libs=2, nan_locus=False):
+    rng = np.random.default_rng(seed)
+    rows = []
+    for i in range(n_cells):
+        for ch in chroms:
+            for j in range(per_chr):
+                rows.append(dict(cell_id="{}{}".format(prefix, (i * 7919) % 1000), chr=ch, start=j * 500000 + 1,
+                                 gc=0.3 + 0.01 * j + 0.001 * CHR.index(ch), library_id="L{}".format(i % n_libs),
+                                 state=int(rng.integers(1, 5)), reads=float(rng.integers(0, 300)),
+                                 clone_id="AB"[i % 2], copy=float(rng.uniform(1, 4))))
+    df = pd.DataFrame(rows).sample(frac=1.0, random_state=seed).reset_index(drop=True)
+    if nan_locus:                   # one locus missing in one cell: dropped for every cell
+        c0 = df.cell_id.iloc[0]
+        df.loc[(df.cell_id == c0) & (df.chr == "2") & (df.start == 1), "reads"] = np.nan
+    return df
+
+
+def _ref_sort(cn):
+    cn = cn.copy()
+    cn["chr"] = cn["chr"].astype(str).astype("category").cat.set_categories(CHR)
+    return cn.sort_values(by=["cell_id", "chr", "start"])
+
+
+def _ref_process(cn_s, cn_g1):
+    """pert_model.py:133-191 in plain pandas (pivot_table / dropna / .T)."""
+    cn_g1 = _ref_sort(cn_g1)
+    cn_s = _ref_sort(cn_s)
+    cn_g1 = cn_g1[cn_g1["reads"].notna()]
+    cn_s = cn_s[cn_s["reads"].notna()]
+    piv = lambda df, col: df.pivot_table(index="cell_id", columns=["chr", "start"], values=col,
+                                         observed=False).dropna(axis=1).T
+    g_r, g_s, s_r, s_s = piv(cn_g1, "reads"), piv(cn_g1, "state"), piv(cn_s, "reads"), piv(cn_s, "state")
+    libs_s = cn_s[["cell_id", "library_id"]].drop_duplicates()
+    libs_g = cn_g1[["cell_id", "library_id"]].drop_duplicates()
+    ids = list(pd.concat([libs_s, libs_g])["library_id"].unique())
+    lut = {v: i for i, v in enumerate(ids)}
+    gam = cn_s[["chr", "start", "gc"]].drop_duplicates().dropna()
+    return dict(cn_s=cn_s, cn_g1=cn_g1, g_r=g_r, g_s=g_s, s_r=s_r, s_s=s_s,
+                libs_s=libs_s["library_id"].map(lut).to_numpy(), libs_g=libs_g["library_id"].map(lut).to_numpy(),
+                ids=ids, gc=gam["gc"].to_numpy(np.float32))
+
+
+@pytest.mark.parametrize("nan_locus", [False, True])
+def test_process_input_data_matches_pandas(nan_locus):
+    s = _table(9, "s", seed=1, nan_locus=nan_locus)
+    g = _table(6, "g", seed=2, n_libs=3, nan_locus=nan_locus)
+    ref = _ref_process(s, g)
+    cn_s, cn_g1, inp = prep.process_input_data(s, g)
+    # sorted long tables: same rows in the same order
+    assert (cn_s.index.to_numpy() == ref["cn_s"].index.to_numpy()).all()
+    assert (cn_g1.index.to_numpy() == ref["cn_g1"].index.to_numpy()).all()
+    np.testing.assert_array_equal(inp.cells_s, ref["s_r"].columns.to_numpy())
+    np.testing.assert_array_equal(inp.cells_g, ref["g_r"].columns.to_numpy())
+    np.testing.assert_array_equal(inp.loci_chr.astype(str), ref["s_r"].index.get_level_values(0).astype(str))
+    np.testing.assert_array_equal(inp.loci_start, ref["s_r"].index.get_level_values(1))
+    t32 = lambda df: df.to_numpy().astype(np.int64).astype(np.float32)
+    np.testing.assert_array_equal(inp.reads_s, t32(ref["s_r"]))
+    np.testing.assert_array_equal(inp.reads_g, t32(ref["g_r"]))
+    np.testing.assert_array_equal(inp.states_g, t32(ref["g_s"]))
+    if not nan_locus:
+        np.testing.assert_array_equal(inp.states_s, t32(ref["s_s"]))
+        np.testing.assert_array_equal(inp.gc, ref["gc"])
+    np.testing.assert_array_equal(inp.libs_s, ref["libs_s"])
+    np.testing.assert_array_equal(inp.libs_g, ref["libs_g"])
+    assert inp.library_ids == ref["ids"]
+
+
+def test_pivot_averages_duplicates_and_drops_nan_keys():
+    df = pd.DataFrame(dict(cell_id=["b", "a", "a", "b", "a", None], chr=["1", "1", "1", "2", "Z", "1"],
+                           start=[1, 1, 1, 1, 1, 1], v=[1.0, 2.0, 4.0, 5.0, 9.0, 7.0]))
+    p = prep.pivot_cells_by_loci(df, "v", "cell_id", "chr", "start")
+    assert list(p.cells) == ["a", "b"]
+    assert list(p.loci_chr) == ["1", "2"]
+    np.testing.assert_array_equal(p.values, [[3.0, 1.0], [np.nan, 5.0]])
+
+
+def test_consensus_clone_profiles_matches_pandas():
+    from scipy.stats import mode
+    g = _table(10, "g", seed=3)
+    g.loc[g.cell_id == g.cell_id.iloc[0], "state"] = 7            # an off-ploidy cell
+    got = prep.consensus_clone_profiles(g, "copy")
+    # compute_consensus_clone_profiles.py:42-88 restated
+    cn = g[g["clone_id"] != "None"].copy()
+    pl = {c: mode(grp["state"], keepdims=False)[0] for c, grp in cn.groupby("cell_id")}
+    cn["ploidy"] = cn["cell_id"].map(pl)
+    pieces = []
+    for _, grp in cn.groupby("clone_id"):
+        keep = grp.groupby("ploidy").size().idxmax()
+        pieces.append(grp[grp["ploidy"] == keep])
+    cn = pd.concat(pieces, ignore_index=True)
+    ref = cn.pivot_table(index=["chr", "start"], columns="clone_id", values="copy", aggfunc="median")
+    ref.index = pd.MultiIndex.from_arrays([ref.index.get_level_values(0).astype(str), ref.index.get_level_values(1)])
+    got.index = pd.MultiIndex.from_arrays([got.index.get_level_values(0).astype(str), got.index.get_level_values(1)])
+    got = got.loc[ref.index, ref.columns]
+    np.testing.assert_allclose(got.to_numpy(), ref.to_numpy())
+
+
+def test_clone_prior_matches_dense_reference():
+    s = _table(8, "s", seed=4)
+    g = _table(6, "g", seed=5)
+    cn_s, cn_g1, inp = prep.process_input_data(s, g)
+    prof = prep.consensus_clone_profiles(cn_g1, "state")
+    eta = prep.build_clone_cn_prior(cn_s, inp.cells_s, inp.loci_chr, inp.loci_start, prof, 1e6, 13)
+    dense = eta.dense()
+    # pert_model.py:285-296: eta[:, n, clone_profile[l]] = weight, ones elsewhere
+    idx = pd.MultiIndex.from_arrays([prof.index.get_level_values(0).astype(str), prof.index.get_level_values(1)])
+    li = idx.get_indexer(pd.MultiIndex.from_arrays([inp.loci_chr.astype(str), inp.loci_start]))
+    for n, cell in enumerate(inp.cells_s):
+        clone = cn_s.loc[cn_s.cell_id == cell, "clone_id"].values[0]
+        st = prof[clone].to_numpy()[li].astype(np.int64)
+        want = np.ones((len(li), 13), np.float32)
+        want[np.arange(len(li)), st] = 1e6
+        np.testing.assert_array_equal(dense[:, n], want)
+
+
+def test_package_output_keys_path_matches_lookup_path():
+    from scdna_replication_tools_amd.pert_model import pert_infer_scRT
+    s = _table(8, "s", seed=6)
+    g = _table(6, "g", seed=7)
+    m = pert_infer_scRT(s, g, cn_prior_method='g1_clones', device='cpu')
+    inp = m.process_input_data()
+    L, N = inp.reads_s.shape
+    rng = np.random.default_rng(0)
+    cn = rng.integers(0, 13, (L, N))
+    rep = rng.integers(0, 2, (L, N))
+    fit = {"expose_tau": rng.uniform(size=N), "expose_u": rng.uniform(size=N), "expose_rho": rng.uniform(size=L),
+           "expose_a": np.array([7.0])}
+    args = (m.cn_s, inp.cells_s, inp.loci_chr, inp.loci_start, cn, rep, fit, np.array([0.7]), [1.0], [2.0])
+    a, sa = m.package_s_output(*args, keys=inp.keys_s)
+    b, sb = m.package_s_output(*args)
+    pd.testing.assert_frame_equal(a, b)
+    pd.testing.assert_frame_equal(sa, sb)
+    # spot check: every row carries its own (locus, cell) decode
+    r = a.iloc[5]
+    n = list(inp.cells_s).index(r["cell_id"])
+    l = [i for i in range(L) if inp.loci_chr[i] == str(r["chr"]) and inp.loci_start[i] == r["start"]][0]
+    assert r["model_cn_state"] == cn[l, n] and r["model_rep_state"] == rep[l, n]

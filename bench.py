@@ -111,6 +111,7 @@ def main():
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     ap.add_argument("--bins-per-tile", type=int, default=0)
     ap.add_argument("--variant", type=int, default=0, help="enumerated-pass kernel: 0 LDS-DMA, 1 register")
+    ap.add_argument("--cells", type=int, default=0, help="override the config's cell count (per job)")
     ap.add_argument("--cpu-cells", type=int, default=128)
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -133,6 +134,9 @@ def main():
     from scdna_replication_tools_amd.sharding import cell_bounds, make_allreduce
 
     n_cells, subdiv, desc = CONFIGS[args.config]
+    if args.cells > 0:
+        n_cells = args.cells
+        desc = "synthetic {} cells x {} bins (--cells override of {})".format(n_cells, 5451 * subdiv, args.config)
     n_total = n_cells * (world if args.scaling == "weak" else 1)
     data = synth(n_total, subdiv, seed=0, device=device)
     L = data["reads"].shape[0]

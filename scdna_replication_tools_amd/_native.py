@@ -12,6 +12,9 @@ from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_voi
 
 LIB_NAME = "libpert_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# A/B measurement hook: PERT_LIB names another build of the same ABI (e.g. a previous
+# kernel version compiled by tools/build_ab.sh); the product default is LIB_PATH.
+LIB_PATH = os.environ.get("PERT_LIB", LIB_PATH)
 
 KIND_STEP1, KIND_STEP2, KIND_STEP3 = 1, 2, 3
 MODE_STEP, MODE_GRAD, MODE_DECODE = 0, 1, 2

@@ -29,6 +29,7 @@ constexpr int kBlock = PERT_BLOCK;
 constexpr int kWaves = kBlock / 64;
 constexpr int kDefaultLT = 32;
 constexpr int kMaxLT = 64;
+constexpr int kEtaLdsFloats = 1024;   // eta tables up to 4 KB are staged in LDS
 constexpr int kBlkSlots = 4;      // loss, d/da, sum delta, sum gdd (step 1)
 constexpr float kHalfLog2PiF = 0.918938533204672742f;
 
@@ -315,6 +316,13 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
 
   const float* __restrict__ params = st.params;
   float* s_bc = s_binp + LT;
+  // the eta table (n_codes x (P+1)) is staged in LDS when it is small (every builder but a
+  // large composite prior): the tail's per-lane row gather is then an LDS read, not a
+  // dependent global load after the forward pass
+  float* s_tab = s_bc + LT * (K1 + 1);
+  const bool etal = !kDecode && pr.n_codes * (P + 1) <= kEtaLdsFloats;
+  if (etal)
+    for (int i = lane; i < pr.n_codes * (P + 1); i += 64) s_tab[i] = pr.eta_table[i];
   // per-bin constants of the tile: constrained rho and the GC features
   for (int i = lane; i < (l1 - l0) * (K1 + 1); i += 64) {
     const int lb = i / (K1 + 1), j = i - lb * (K1 + 1);
@@ -404,11 +412,18 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
       float zt[P];
 #pragma unroll
       for (int k = 0; k < P; ++k) zt[k] = sb[k * 64 + lane];
-      const float* row = pr.eta_table + (size_t)code * (P + 1);
-      float em1[P];
+      float em1[P], S1;
+      if (etal) {
+        const float* row = s_tab + code * (P + 1);
 #pragma unroll
-      for (int k = 0; k < P; ++k) em1[k] = row[k];
-      const float S1 = row[P];
+        for (int k = 0; k < P; ++k) em1[k] = row[k];
+        S1 = row[P];
+      } else {
+        const float* row = pr.eta_table + (size_t)code * (P + 1);
+#pragma unroll
+        for (int k = 0; k < P; ++k) em1[k] = row[k];
+        S1 = row[P];
+      }
       float gz[P];
       const float dirv = enum_tail<P>(o, zt, em1, S1, gz);
       if (valid) {
@@ -626,6 +641,7 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(pert_problem pr, pert_
 #pragma unroll
     for (int k = 0; k <= PERT_MAX_K1; ++k) A[k] = 0.0;
     if (in_range) {
+#pragma unroll 4
       for (int bt = grp; bt < n_bt; bt += kFG) {
         const float* cp = st.cell_part + (size_t)bt * (K1 + 1) * N + n;
 #pragma unroll
@@ -694,22 +710,39 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(pert_problem pr, pert_
       if (k < K1) gc[lay.off_beta + k * N + n] = -dB[k];
     gc[lay.off_tau + n] = -dTau * dtau_dz;
   }
-  // per-library sums for beta_stds (and beta_means in step 1), plus the prior log densities
+  // per-library sums for beta_stds (and beta_means in step 1), plus the prior log densities:
+  // every slot reduced by wave shuffles, one LDS round, fixed order
   const int nslot = 2 * nl * K1 + 1;
   double* out = st.cellblk_part + (size_t)blockIdx.x * nslot;
-  for (int li = 0; li < nl; ++li) {
-    for (int k = 0; k < K1; ++k) {
-      const bool mine = valid && lib == li;
-      const double s1 = block_sum_d(mine ? (double)dzbs[k] : 0.0, s_red);
-      const double s2 = step1 ? block_sum_d(mine ? (double)dbm[k] : 0.0, s_red) : 0.0;
-      if (tid == 0) {
-        out[li * K1 + k] = s1;
-        out[nl * K1 + li * K1 + k] = s2;
+  __shared__ double s_fs[kWaves][64];
+  const int lane = tid & 63, wave = tid >> 6;
+  for (int s0 = 0; s0 < nslot; s0 += 64) {
+    for (int sl = s0; sl < min(nslot, s0 + 64); ++sl) {
+      double val;
+      if (sl < 2 * nl * K1) {
+        const int half = sl / (nl * K1), r = sl - half * nl * K1;
+        const int li = r / K1, k = r - li * K1;
+        const bool mine = valid && lib == li && (half == 0 || step1);
+        float fv = 0.0f;
+#pragma unroll
+        for (int kk = 0; kk < PERT_MAX_K1; ++kk)
+          if (kk == k) fv = half == 0 ? dzbs[kk] : dbm[kk];
+        val = mine ? (double)fv : 0.0;
+      } else {
+        val = lp;
       }
+      val = wave_sum_d(val);
+      if (lane == 0) s_fs[wave][sl - s0] = val;
     }
+    __syncthreads();
+    if (tid < min(nslot, s0 + 64) - s0) {
+      double t = 0.0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) t += s_fs[w][tid];
+      out[s0 + tid] = t;
+    }
+    __syncthreads();
   }
-  const double slp = block_sum_d(lp, s_red);
-  if (tid == 0) out[2 * nl * K1] = slp;
 }
 
 // Global sums: one 1024-thread workgroup, fixed order.
@@ -732,34 +765,53 @@ __global__ void __launch_bounds__(kScalarBlock) scalar_kernel(pert_problem pr, p
   const int K1 = pr.K1, nl = pr.n_libs;
   const pert_layout lay = st.lay;
   const int kind = pr.kind;
-  __shared__ double s_red[kScalarBlock / 64];
+  constexpr int kSW = kScalarBlock / 64;
+  __shared__ double s_red4[kSW][kBlkSlots];
+  __shared__ double s_slot[64];
+  const int lane = tid & 63, wave = tid >> 6;
+  // (1) the enum/obs block partials: all 1024 threads, double4 per block, one LDS round
   double v[kBlkSlots] = {0.0, 0.0, 0.0, 0.0};
   const double4* bp4 = reinterpret_cast<const double4*>(st.blk_part);
   for (int b = tid; b < n_blk; b += kScalarBlock) {
     const double4 q = bp4[b];
     v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
   }
+#pragma unroll
+  for (int j = 0; j < kBlkSlots; ++j) v[j] = wave_sum_d(v[j]);
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < kBlkSlots; ++j) s_red4[wave][j] = v[j];
+  }
+  // (2) the finalize cell-block partials: one wave per slot (fixed order)
+  const int nslot = 2 * nl * K1 + 1;
+  for (int sl = wave; sl < nslot; sl += kSW) {
+    double acc = 0.0;
+    for (int b = lane; b < n_cblk; b += 64) acc += st.cellblk_part[(size_t)b * nslot + sl];
+    acc = wave_sum_d(acc);
+    if (lane == 0) s_slot[sl] = acc;
+  }
+  __syncthreads();
+  if (tid != 0) return;
   double tot[kBlkSlots];
 #pragma unroll
-  for (int j = 0; j < kBlkSlots; ++j) tot[j] = block_sum_d1024(v[j], s_red);
-
-  const int nslot = 2 * nl * K1 + 1;
+  for (int j = 0; j < kBlkSlots; ++j) {
+    double t = 0.0;
+    for (int w = 0; w < kSW; ++w) t += s_red4[w][j];
+    tot[j] = t;
+  }
   double elbo = tot[0];
-  // cell-block partials
-  for (int s = 0; s < nslot; ++s) {
-    double acc = 0.0;
-    for (int b = tid; b < n_cblk; b += kScalarBlock) acc += st.cellblk_part[(size_t)b * nslot + s];
-    const double S = block_sum_d1024(acc, s_red);
-    if (s < nl * K1) {
-      if (tid == 0) st.grad_shared[lay.off_bstds + s] = -S;
-    } else if (s < 2 * nl * K1) {
+  for (int sl = 0; sl < nslot; ++sl) {
+    const double S = s_slot[sl];
+    if (sl < nl * K1) {
+      st.grad_shared[lay.off_bstds + sl] = -S;
+    } else if (sl < 2 * nl * K1) {
+      const int j = sl - nl * K1;
       if (kind == PERT_KIND_STEP1) {
-        const int j = s - nl * K1;
         const double bm = st.params[lay.off_bmeans + j];
         // beta_means ~ N(0, 1) (:560): prior gradient -bm added once (root)
-        if (tid == 0) st.grad_shared[lay.off_bmeans + j] = -(S + (pr.is_root ? -bm : 0.0));
-      } else if (tid == 0) {
-        st.grad_shared[lay.off_bmeans + (s - nl * K1)] = 0.0;
+        st.grad_shared[lay.off_bmeans + j] = -(S + (pr.is_root ? -bm : 0.0));
+      } else {
+        st.grad_shared[lay.off_bmeans + j] = 0.0;
       }
     } else {
       elbo += S;
@@ -859,7 +911,8 @@ bool problem_ok(const pert_problem* p) {
 size_t dma_lds_bytes(int P, int mode, const pert_state& st, const pert_problem& pr) {
   const int ZF = P * 64, SF = ZF + 96;
   const int lt = st.bins_per_tile;
-  return sizeof(float) * (size_t)(2 * SF + (mode == PERT_MODE_STEP ? 2 * ZF : 0) + lt + lt * (pr.K1 + 1));
+  const int tab = (mode != PERT_MODE_DECODE && pr.n_codes * (P + 1) <= kEtaLdsFloats) ? pr.n_codes * (P + 1) : 0;
+  return sizeof(float) * (size_t)(2 * SF + (mode == PERT_MODE_STEP ? 2 * ZF : 0) + lt + lt * (pr.K1 + 1) + tab);
 }
 
 // cells per tile of the enumerated pass: 64 for the LDS-DMA kernel (variant 0), 256 otherwise
@@ -990,6 +1043,7 @@ int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream) 
                      n_bt, n_ct);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_status(e);
+  if (2 * prob->n_libs * prob->K1 + 1 > 64) return PERT_E_ARG;       // scalar_kernel's slot table
   hipLaunchKernelGGL(scalar_kernel, dim3(1), dim3(kScalarBlock), 0, stream, *prob, s2, n_bt * n_ct, n_cblk);
   return hip_status(hipGetLastError());
 }

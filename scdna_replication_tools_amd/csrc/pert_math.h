@@ -88,6 +88,22 @@ PERT_HD void nb_lgdiff_asym(float d, float x, float invx, float& lam, float& psi
         + 0.00833333333333333333f * (rz4 - r4) - 0.00396825396825396825f * (rz4 * rz2 - r4 * r2);
 }
 
+// nb_lgdiff_asym for d = chi D >= 8 with the per-(bin, cell) invariants hoisted out of
+// the chi loop: r = 1/d = (1/D)(1/chi) (one v_rcp per cell.bin instead of per chi) and
+// log1p(d/x) = log1p(x/d) + log(d/x), log(d/x) = log(chi) + (log D - log x) (no second
+// v_log per chi).  ldxc = log(d/x) (any finite value when x == 0: it is multiplied by x).
+PERT_HD void nb_lgdiff_asym_hoisted(float d, float r, float x, float ldxc, float& lam, float& psi) {
+  const float zs = d + x;
+  const float rz = frcp(zs);
+  const float l1 = log1p_corr(x * r, d * rz);         // log1p(x/d)
+  const float l2 = l1 + ldxc;                         // log1p(d/x)
+  lam = (d - 0.5f) * l1 + x * l2 + (stirling_rem(rz) - stirling_rem(r));
+  const float r2 = r * r, rz2 = rz * rz;
+  const float r4 = r2 * r2, rz4 = rz2 * rz2;
+  psi = l1 - 0.5f * (rz - r) - 0.0833333333333333333f * (rz2 - r2)
+        + 0.00833333333333333333f * (rz4 - r4) - 0.00396825396825396825f * (rz4 * rz2 - r4 * r2);
+}
+
 PERT_HD void nb_lgdiff(float d, float x, float invx, float& lam, float& psi) {
   float corr_l = 0.0f, corr_p = 0.0f;
   if (d < 8.0f) {
@@ -131,6 +147,16 @@ PERT_HD float lambda_delta1(float x, float invx) {
   nb_lgdiff(1.0f, x, invx, lam, psi);
   return lam;
 }
+
+// log(k) for k = 0..31 (k = 0 unused)
+constexpr float kLogInt[32] = {
+    0.0f, 0.0f, 0.693147180559945f, 1.098612288668110f, 1.386294361119891f, 1.609437912434100f,
+    1.791759469228055f, 1.945910149055313f, 2.079441541679836f, 2.197224577336220f, 2.302585092994046f,
+    2.397895272798371f, 2.484906649788000f, 2.564949357461537f, 2.639057329615259f, 2.708050201102210f,
+    2.772588722239781f, 2.833213344056216f, 2.890371757896165f, 2.944438979166440f, 2.995732273553991f,
+    3.044522437723423f, 3.091042453358316f, 3.135494215929150f, 3.178053830347946f, 3.218875824868201f,
+    3.258096538021482f, 3.295836866004329f, 3.332204510175204f, 3.367295829986474f, 3.401197381662155f,
+    3.433987204485146f};
 
 // Number of CN states P is a compile-time constant of every kernel; chi = c (1 + r)
 // takes the values 0..P-1 (r = 0) and the even values 0..2P-2 (r = 1).
@@ -208,12 +234,14 @@ PERT_HD void enum_forward(float x, float invx, const float (&z)[P], float log1m_
   if (D >= 8.0f) {
     // every delta = chi D >= 8: straight-line asymptotic series, no clamp, no shift --
     // one basic block, so the 2P-2 independent chains interleave (ILP)
+    const float rD = frcp(D);
+    const float ldx = x > 0.0f ? flog(D) - flog(x) : 0.0f;
 #pragma unroll
     for (int chi = 1; chi < 2 * P - 1; ++chi) {
       if (!chi_needed<P>(chi)) continue;
       const float d = (float)chi * D;
       float lam, psi;
-      nb_lgdiff_asym(d, x, invx, lam, psi);
+      nb_lgdiff_asym_hoisted(d, rD * (1.0f / (float)chi), x, ldx + kLogInt[chi], lam, psi);
       const float nchi = d * log1m_lam + lam;
       Bc[chi] = (float)chi * (log1m_lam + psi);
       if (chi < P) s[chi] += nchi;

@@ -19,6 +19,7 @@ Everything runs through libpert_hip.so; there is no host fallback.
 from __future__ import annotations
 
 import ctypes
+import contextlib
 import math
 from dataclasses import dataclass
 from typing import Callable, Dict, Optional
@@ -169,6 +170,21 @@ def _ptr(t: Optional[torch.Tensor]) -> int:
     return 0 if t is None else int(t.data_ptr())
 
 
+def auto_bins_per_tile(kind: int, L: int, ldn: int, variant: int = 0, n_cu: int = 256) -> int:
+    """Bins per workgroup tile of the LDS-DMA enumerated pass: the longest of 64/32/16/8
+    that still gives >= 3 one-wave workgroups per wave slot of the chip (256 CUs x 8),
+    so long tiles amortise the per-tile prologue on big shards and short tiles keep the
+    chip full on small ones (strong-scaling shards)."""
+    if kind == nat.KIND_STEP1 or variant != 0:
+        return 32
+    slots = n_cu * 8
+    n_ct = ldn // 64
+    for lt in (64, 32, 16):
+        if n_ct * (-(-L // lt)) >= 3 * slots:
+            return lt
+    return 8
+
+
 class PertShard:
     """One fit (kind 1/2/3) over one contiguous cell shard, resident on one GPU."""
 
@@ -184,6 +200,8 @@ class PertShard:
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise ValueError("PertShard needs a GPU device (got {})".format(self.device))
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         reads = np.asarray(reads)
         L, N = reads.shape
         self.L, self.N, self.P, self.K, self.K1, self.n_libs = L, N, int(P), int(K), int(K) + 1, int(n_libs)
@@ -263,6 +281,8 @@ class PertShard:
         self.cn_out = torch.zeros((L, ldn), dtype=torch.uint8, device=dev)
         self.rep_out = torch.zeros((L, ldn), dtype=torch.uint8, device=dev)
 
+        if bins_per_tile <= 0:
+            bins_per_tile = auto_bins_per_tile(self.kind, L, ldn, variant)
         ncp, nbp, nblk, ncb = nat.workspace_sizes(self.kind, L, N, self.K1, self.n_libs, bins_per_tile)
         self.cell_part = torch.zeros(ncp, **f32)
         self.bin_part = torch.zeros(nbp, **f32)
@@ -397,9 +417,15 @@ class PertShard:
         self._hp.step_size = self.lr / (1.0 - b1 ** t)
         self._hp.inv_bc2_sqrt = 1.0 / math.sqrt(1.0 - b2 ** t)
 
+    def _dev(self):
+        """Device guard only when the current device differs (the common case costs nothing)."""
+        if torch.cuda.current_device() == self.device.index:
+            return contextlib.nullcontext()
+        return torch.cuda.device(self.device)
+
     def _pass(self, mode: int):
         s = self._stream()
-        with torch.cuda.device(self.device):
+        with self._dev():
             if self.kind == nat.KIND_STEP1:
                 nat.check(self.lib.pert_obs_pass(ctypes.byref(self._prob), ctypes.byref(self._state), s),
                           "pert_obs_pass")
@@ -408,7 +434,7 @@ class PertShard:
                                                   ctypes.byref(self._hp), mode, s), "pert_enum_pass")
 
     def _finalize(self):
-        with torch.cuda.device(self.device):
+        with self._dev():
             nat.check(self.lib.pert_finalize(ctypes.byref(self._prob), ctypes.byref(self._state), self._stream()),
                       "pert_finalize")
         if self.allreduce is not None:
@@ -428,7 +454,7 @@ class PertShard:
         else:
             self._pass(nat.MODE_STEP)
         self._finalize()
-        with torch.cuda.device(self.device):
+        with self._dev():
             nat.check(self.lib.pert_adam(ctypes.byref(self._prob), ctypes.byref(self._state),
                                          ctypes.byref(self._hp), self._stream()), "pert_adam")
         if self.pi_block is not None:

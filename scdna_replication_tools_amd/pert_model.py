@@ -112,7 +112,7 @@ class pert_infer_scRT():
             return prep.build_g1_cells_prior(inp, self.cn_s, self.cn_g1, w, P, self.cell_col, self.clone_col)
         if m == 'g1_clones':
             return prep.build_clone_cn_prior(self.cn_s, inp.cells_s, inp.loci_chr, inp.loci_start, profiles, w, P,
-                                             self.cell_col, self.clone_col)
+                                             self.cell_col, self.clone_col, keys=inp.keys_s)
         if m == 'g1_composite':
             return prep.build_composite_cn_prior(inp, self.cn_s, self.cn_g1, profiles, P, J=self.J,
                                                  cell_col=self.cell_col, clone_col=self.clone_col,
@@ -155,7 +155,7 @@ class pert_infer_scRT():
         n_libs = self.L
         profiles = prep.consensus_clone_profiles(
             self.cn_g1, self.cn_state_col, clone_col=self.clone_col, cell_col=self.cell_col,
-            chr_col=self.chr_col, start_col=self.start_col, cn_state_col=self.cn_state_col)
+            chr_col=self.chr_col, start_col=self.start_col, cn_state_col=self.cn_state_col, keys=inp.keys_g)
         etas = self.build_etas(inp, profiles)
         self.timings["prep"] = time.perf_counter() - tic
 
@@ -199,7 +199,7 @@ class pert_infer_scRT():
             # ---- step 3: G1 cells with rho, a frozen (:834-896)
             tic = time.perf_counter()
             etas2 = prep.build_clone_cn_prior(self.cn_g1, inp.cells_g, inp.loci_chr, inp.loci_start, profiles,
-                                              self.cn_prior_weight, P, self.cell_col, self.clone_col)
+                                              self.cn_prior_weight, P, self.cell_col, self.clone_col, keys=inp.keys_g)
             t_init2, _, _ = self.guess_times(inp.reads_g, etas2.argmax_states())
             ploidy2 = etas2.argmax_states().astype(np.float32).mean(0)
             self.timings["prep_step3"] = time.perf_counter() - tic
@@ -239,14 +239,17 @@ class pert_infer_scRT():
             li = locus_index.get_indexer(pd.MultiIndex.from_arrays(
                 [cn[self.chr_col].astype(str).to_numpy(), cn[self.start_col].to_numpy()]))
         keep = (ci >= 0) & (li >= 0)
-        out = cn.loc[keep].copy() if not keep.all() else cn.copy()
+        base = cn.loc[keep] if not keep.all() else cn
         ci, li = ci[keep], li[keep]
-        out['model_cn_state'] = model_cn[li, ci].astype(np.int64)
-        out['model_rep_state'] = model_rep[li, ci].astype(np.float32)
-        out['model_tau'] = np.asarray(fit["expose_tau"], dtype=np.float32)[ci]
-        out['model_u'] = np.asarray(fit["expose_u"], dtype=np.float32)[ci]
-        out['model_rho'] = np.asarray(fit["expose_rho"], dtype=np.float32).reshape(-1)[li]
-        out = out.reset_index(drop=True)
+        model = pd.DataFrame({
+            'model_cn_state': model_cn[li, ci].astype(np.int64),
+            'model_rep_state': model_rep[li, ci].astype(np.float32),
+            'model_tau': np.asarray(fit["expose_tau"], dtype=np.float32)[ci],
+            'model_u': np.asarray(fit["expose_u"], dtype=np.float32)[ci],
+            'model_rho': np.asarray(fit["expose_rho"], dtype=np.float32).reshape(-1)[li],
+        })
+        # new columns side by side with the (sorted) input rows, without copying its blocks
+        out = pd.concat([base.reset_index(drop=True), model], axis=1, copy=False)
         supp = pd.concat([
             pd.DataFrame({'param': ['model_lambda'], 'level': ['all'], 'value': [float(lambda_fit[0])]}),
             pd.DataFrame({'param': ['model_a'], 'level': ['all'], 'value': [float(np.asarray(fit["expose_a"])[0])]}),

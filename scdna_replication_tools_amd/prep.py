@@ -28,10 +28,17 @@ CHR_ORDER = [str(i + 1) for i in range(22)] + ["X", "Y"]
 
 
 def _chr_codes(chrc: pd.Series) -> np.ndarray:
-    """Chromosome category codes in CHR_ORDER (-1 for labels outside it / NaN)."""
-    if isinstance(chrc.dtype, pd.CategoricalDtype) and list(chrc.cat.categories) == CHR_ORDER:
-        return chrc.cat.codes.to_numpy().astype(np.int64)
-    return chrc.astype(str).astype(pd.CategoricalDtype(CHR_ORDER)).cat.codes.to_numpy().astype(np.int64)
+    """Chromosome category codes in CHR_ORDER (-1 for labels outside it / NaN): the
+    labels are factorised first and only the few uniques go through ``str``."""
+    if isinstance(chrc.dtype, pd.CategoricalDtype):
+        cats = np.asarray(chrc.cat.categories)
+        codes = chrc.cat.codes.to_numpy().astype(np.int64)
+    else:
+        codes, cats = pd.factorize(chrc.to_numpy())
+        codes = codes.astype(np.int64)
+    pos = {c: i for i, c in enumerate(CHR_ORDER)}
+    lut = np.array([pos.get(str(c), -1) for c in cats] + [-1], dtype=np.int64)
+    return lut[np.where(codes >= 0, codes, len(cats))]
 
 
 def _sorted_codes(values) -> tuple:
@@ -58,7 +65,10 @@ def _sorted_table(cn: pd.DataFrame, cell_col: str, chr_col: str, start_col: str,
         order = np.lexsort((st_key, chk, cck))
     if notna_col is not None:
         order = order[cn[notna_col].notna().to_numpy()[order]]
-    out = cn.take(order)
+    if order.size == len(cn) and (order.size == 0 or (order[1:] > order[:-1]).all()):
+        out = cn.copy()                                  # already sorted and complete: no gather
+    else:
+        out = cn.take(order)
     out[chr_col] = pd.Categorical.from_codes(ch[order], categories=CHR_ORDER)
     return out, TableKeys.from_codes(cc[order], cells, ch[order], st[order])
 
@@ -306,7 +316,7 @@ def _group_median(group: np.ndarray, values: np.ndarray, n_groups: int) -> np.nd
 
 
 def consensus_clone_profiles(cn: pd.DataFrame, col_name: str, clone_col="clone_id", cell_col="cell_id",
-                             chr_col="chr", start_col="start", cn_state_col="state") -> pd.DataFrame:
+                             chr_col="chr", start_col="start", cn_state_col="state", keys=None) -> pd.DataFrame:
     """compute_consensus_clone_profiles (:42-88): median of ``col_name`` per (locus, clone)
     over the clone's majority-ploidy cells; index (chr, start) sorted as pivot_table sorts
     it, columns the sorted clone ids.  Integer codes, row masks and one lexsort; the long
@@ -317,7 +327,10 @@ def consensus_clone_profiles(cn: pd.DataFrame, col_name: str, clone_col="clone_i
         kc = np.where(kc == bad, -1, kc)
     rows = kc >= 0
     if cn_state_col is not None:
-        cc, cells = _sorted_codes(cn[cell_col].to_numpy())
+        if keys is not None and len(keys.cell_code) == len(cn):
+            cc, cells = keys.cell_code, keys.cells
+        else:
+            cc, cells = _sorted_codes(cn[cell_col].to_numpy())
         cc = np.where(rows, cc, -1)
         rows &= _majority_ploidy_rows(cn, clone_col, cell_col, cn_state_col, cc, len(cells), kc, len(ku))
     hc, hu = pd.factorize(cn[chr_col])
@@ -336,8 +349,19 @@ def consensus_clone_profiles(cn: pd.DataFrame, col_name: str, clone_col="clone_i
     return prof.sort_index()
 
 
-def first_clone(cn: pd.DataFrame, cells, cell_col="cell_id", clone_col="clone_id") -> np.ndarray:
-    """cn.loc[cn[cell]==id][clone].values[0] for every id (pert_model.py:289-290)."""
+def first_clone(cn: pd.DataFrame, cells, cell_col="cell_id", clone_col="clone_id", keys=None) -> np.ndarray:
+    """cn.loc[cn[cell]==id][clone].values[0] for every id (pert_model.py:289-290).
+    ``keys``: the table's TableKeys (row order), to find first rows by cell code."""
+    if keys is not None and len(keys.cell_code) == len(cn):
+        ok = keys.cell_code >= 0
+        _, first = np.unique(keys.cell_code[ok], return_index=True)
+        rows = np.flatnonzero(ok)[first]
+        clone_of = cn[clone_col].to_numpy()[rows]                  # per keys.cells
+        pos = pd.Index(keys.cells).get_indexer(np.asarray(cells))
+        out = np.empty(len(pos), dtype=object)
+        out[pos >= 0] = clone_of[pos[pos >= 0]]
+        out[pos < 0] = np.nan
+        return out
     f = cn[[cell_col, clone_col]].drop_duplicates(cell_col).set_index(cell_col)[clone_col]
     return f.reindex(cells).to_numpy()
 
@@ -360,9 +384,9 @@ def build_cn_prior(states, weight: float, P: int) -> EtaCodebook:
 
 
 def build_clone_cn_prior(cn: pd.DataFrame, cells, loci_chr, loci_start, profiles: pd.DataFrame, weight: float,
-                         P: int, cell_col="cell_id", clone_col="clone_id") -> EtaCodebook:
+                         P: int, cell_col="cell_id", clone_col="clone_id", keys=None) -> EtaCodebook:
     """pert_model.py:285-296: the consensus clone profile (int64-truncated) as prior state."""
-    clones = first_clone(cn, cells, cell_col, clone_col)
+    clones = first_clone(cn, cells, cell_col, clone_col, keys)
     prof = _profile_matrix(profiles, clones, loci_chr, loci_start)
     return build_cn_prior(prof.astype(np.int64), weight, P)
 

@@ -30,6 +30,7 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kDefaultLT = 32;
 constexpr int kMaxLT = 64;
 constexpr int kEtaLdsFloats = 1024;   // eta tables up to 4 KB are staged in LDS
+constexpr int kFoldMin = 32;           // finalize folds the per-cell partials above this many bin tiles
 constexpr int kBlkSlots = 4;      // loss, d/da, sum delta, sum gdd (step 1)
 constexpr float kHalfLog2PiF = 0.918938533204672742f;
 
@@ -587,8 +588,34 @@ __global__ void __launch_bounds__(kBlock) obs_kernel(pert_problem pr, pert_state
 // ------------------------------------------------------------------------------------------
 // Per-cell and per-bin reductions + priors of the non-enumerated sites.
 // Blocks [0, n_cblk) handle 256 cells each; blocks [n_cblk, n_cblk + n_lblk) 256 bins each.
+// Per-cell partials [n_bt][K1+1][N] folded by kFoldT bin tiles: one thread per (cell,
+// chunk of kFoldT tiles) with all its loads independent, so the whole workspace is in
+// flight at once (a small shard has few cells but many bin tiles; the per-cell loop of
+// finalize_kernel alone is a latency chain there).  Output [ceil(n_bt/kFoldT)][K1+1][N].
+constexpr int kFoldT = 8;
+__global__ void __launch_bounds__(kBlock) fold_cell_part_kernel(const float* __restrict__ in,
+                                                               float* __restrict__ out, int N, int n_bt,
+                                                               int K1p1) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + lane;
+  const int c = blockIdx.y * kWaves + w;
+  const int b0 = c * kFoldT;
+  if (n >= N || b0 >= n_bt) return;
+  const int nb = min(kFoldT, n_bt - b0);
+  for (int k = 0; k < K1p1; ++k) {
+    float v[kFoldT];
+#pragma unroll
+    for (int i = 0; i < kFoldT; ++i) v[i] = i < nb ? in[((size_t)(b0 + i) * K1p1 + k) * N + n] : 0.0f;
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < kFoldT; ++i) acc += (double)v[i];
+    out[((size_t)c * K1p1 + k) * N + n] = (float)acc;
+  }
+}
+
 __global__ void __launch_bounds__(kBlock) finalize_kernel(pert_problem pr, pert_state st,
-                                                          int n_cblk, int n_bt, int n_ct) {
+                                                          int n_cblk, int n_bt, int n_ct,
+                                                          const float* __restrict__ cell_part) {
   const int tid = threadIdx.x;
   const int N = pr.N, K1 = pr.K1, L = pr.L, nl = pr.n_libs;
   const pert_layout lay = st.lay;
@@ -643,7 +670,7 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(pert_problem pr, pert_
     if (in_range) {
 #pragma unroll 4
       for (int bt = grp; bt < n_bt; bt += kFG) {
-        const float* cp = st.cell_part + (size_t)bt * (K1 + 1) * N + n;
+        const float* cp = cell_part + (size_t)bt * (K1 + 1) * N + n;
 #pragma unroll
         for (int k = 0; k <= PERT_MAX_K1; ++k)
           if (k <= K1) A[k] += (double)cp[(size_t)k * N];
@@ -988,7 +1015,8 @@ int pert_workspace_sizes(int32_t kind, int32_t L, int32_t N, int32_t K1, int32_t
   const int lt = tile_bins(&tmp);
   const int64_t ldn = (N + kBlock - 1) / kBlock * kBlock;
   const int64_t n_bt = (L + lt - 1) / lt, n_ct = ldn / 64;     // sized for the 64-cell tiles
-  if (n_cell_part) *n_cell_part = n_bt * (K1 + 1) * (int64_t)N;
+  const int64_t n_fold = n_bt > kFoldMin ? (n_bt + kFoldT - 1) / kFoldT : 0;   // folded copy (finalize)
+  if (n_cell_part) *n_cell_part = (n_bt + n_fold) * (K1 + 1) * (int64_t)N;
   if (n_bin_part) *n_bin_part = n_ct * (int64_t)L;
   if (n_blk_part) *n_blk_part = n_bt * n_ct * kBlkSlots;
   if (n_cellblk_part) *n_cellblk_part = ((N + 31) / 32) * (2 * (int64_t)n_libs * K1 + 1);
@@ -1039,8 +1067,19 @@ int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream) 
   const int n_bt = (prob->L + lt - 1) / lt;
   const int n_lblk = (prob->L + 31) / 32;
   const int n_cblk = (prob->N + 31) / 32;
+  const float* cp = s2.cell_part;
+  int n_bt_f = n_bt;
+  if (n_bt > kFoldMin) {
+    n_bt_f = (n_bt + kFoldT - 1) / kFoldT;
+    float* folded = s2.cell_part + (size_t)n_bt * (prob->K1 + 1) * prob->N;
+    hipLaunchKernelGGL(fold_cell_part_kernel, dim3((prob->N + 63) / 64, (n_bt_f + kWaves - 1) / kWaves),
+                       dim3(kBlock), 0, stream, s2.cell_part, folded, prob->N, n_bt, prob->K1 + 1);
+    hipError_t e0 = hipGetLastError();
+    if (e0 != hipSuccess) return hip_status(e0);
+    cp = folded;
+  }
   hipLaunchKernelGGL(finalize_kernel, dim3(n_cblk + n_lblk), dim3(kBlock), 0, stream, *prob, s2, n_cblk,
-                     n_bt, n_ct);
+                     n_bt_f, n_ct, cp);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_status(e);
   if (2 * prob->n_libs * prob->K1 + 1 > 64) return PERT_E_ARG;       // scalar_kernel's slot table

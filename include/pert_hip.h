@@ -116,6 +116,22 @@ typedef struct {
   double* cellblk_part;
   int32_t bins_per_tile;           /* LT; 0 = library default */
   int32_t variant;                 /* enumerated-pass kernel: 0 LDS-DMA streamed (default), 1 register pipelined */
+  /* Device-side SVI loop control (the loop of pert_model.py:742-758, :800-816, :867-883).
+   * loop_ctl == NULL disables it.  Otherwise pert_adam records the loss of iteration
+   * `step` (after the cross-rank all-reduce) into loop_rec and evaluates the reference's
+   * stopping rule on the device: rel-tol plateau once step >= min_iter (:749-753), then
+   * NaN (:755-758); on a stop it sets loop_ctl[0] = step.  Every PERT_MODE_STEP /
+   * obs / finalize / adam launch of a later step is then a no-op, so the host can queue
+   * iterations ahead without a per-step synchronisation and the fit still stops after
+   * exactly the iteration the reference stops after. */
+  int32_t* loop_ctl;               /* [2]: stop_at (-1 while running), reason (1 rel_tol, 2 NaN) */
+  double* loop_rec;                /* [max_iter][2]: loss of each step, stop_at after it */
+  const double* loss_offset;       /* [max_iter] or NULL: per-step loss term kept on the host side
+                                      of the ABI (step 1's canonical pi block) */
+  double loss_const;               /* loss = grad_shared[n_shared] - loss_const - loss_offset[step] */
+  double rel_tol;
+  int32_t min_iter;
+  int32_t step;                    /* 0-based iteration index of this launch sequence */
 } pert_state;
 
 typedef struct {
@@ -132,6 +148,13 @@ int pert_make_layout(int32_t L, int32_t N, int32_t K1, int32_t n_libs, pert_layo
 int pert_workspace_sizes(int32_t kind, int32_t L, int32_t N, int32_t K1, int32_t n_libs,
                          int32_t bins_per_tile, int64_t* n_cell_part, int64_t* n_bin_part,
                          int64_t* n_blk_part, int64_t* n_cellblk_part);
+
+/* Bins per workgroup tile for the enumerated pass of this shard on the current device:
+ * the tile length in [8, 64] whose grid (ldn/64 cell tiles x ceil(L/LT) bin tiles) best
+ * fills whole rounds of the device's resident wave slots (occupancy queried for the
+ * kernel instance and its LDS at that length), so a small shard does not end on a
+ * partly filled last round.  Written to *out; steps 2/3 only (step 1 uses the default). */
+int pert_auto_bins_per_tile(const pert_problem* prob, int32_t variant, int32_t* out);
 
 /* Enumerated (steps 2/3) pass over every (bin, cell) of the shard.
  * Replaces the JitTraceEnum_ELBO forward + autograd backward of pert_model.py:801 / :868,

@@ -24,7 +24,7 @@ BLOCK = 256
 
 # every symbol include/pert_hip.h declares
 EXPORTED_SYMBOLS = (
-    "pert_make_layout", "pert_workspace_sizes", "pert_enum_pass", "pert_obs_pass",
+    "pert_make_layout", "pert_workspace_sizes", "pert_auto_bins_per_tile", "pert_enum_pass", "pert_obs_pass",
     "pert_finalize", "pert_adam", "pert_selftest_nb_lgdiff_host",
     "pert_selftest_nb_lgdiff_device", "pert_selftest_enum_cellbin_host", "pert_version",
 )
@@ -61,6 +61,8 @@ class PertState(ctypes.Structure):
         ("cell_part", c_void_p), ("bin_part", c_void_p), ("blk_part", c_void_p),
         ("cellblk_part", c_void_p),
         ("bins_per_tile", c_int32), ("variant", c_int32),
+        ("loop_ctl", c_void_p), ("loop_rec", c_void_p), ("loss_offset", c_void_p),
+        ("loss_const", c_double), ("rel_tol", c_double), ("min_iter", c_int32), ("step", c_int32),
     ]
 
 
@@ -95,6 +97,7 @@ def lib():
     handle.pert_make_layout.argtypes = [i32, i32, i32, i32, POINTER(PertLayout)]
     handle.pert_workspace_sizes.argtypes = [i32, i32, i32, i32, i32, i32, POINTER(i64), POINTER(i64),
                                             POINTER(i64), POINTER(i64)]
+    handle.pert_auto_bins_per_tile.argtypes = [POINTER(PertProblem), i32, POINTER(i32)]
     handle.pert_enum_pass.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams),
                                       i32, c_void_p]
     handle.pert_obs_pass.argtypes = [POINTER(PertProblem), POINTER(PertState), c_void_p]
@@ -130,6 +133,14 @@ def workspace_sizes(kind: int, L: int, N: int, K1: int, n_libs: int, bins_per_ti
     check(lib().pert_workspace_sizes(kind, L, N, K1, n_libs, bins_per_tile, *[ctypes.byref(o) for o in out]),
           "pert_workspace_sizes")
     return tuple(int(o.value) for o in out)
+
+
+def auto_bins_per_tile(prob: PertProblem, variant: int = 0) -> int:
+    """pert_auto_bins_per_tile: occupancy-aware tile length on the current device."""
+    out = c_int32()
+    check(lib().pert_auto_bins_per_tile(ctypes.byref(prob), int(variant), ctypes.byref(out)),
+          "pert_auto_bins_per_tile")
+    return int(out.value)
 
 
 def _fptr(a):

@@ -30,7 +30,6 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kDefaultLT = 32;
 constexpr int kMaxLT = 64;
 constexpr int kEtaLdsFloats = 1024;   // eta tables up to 4 KB are staged in LDS
-constexpr int kFoldMin = 32;           // finalize folds the per-cell partials above this many bin tiles
 constexpr int kBlkSlots = 4;      // loss, d/da, sum delta, sum gdd (step 1)
 constexpr float kHalfLog2PiF = 0.918938533204672742f;
 
@@ -64,12 +63,22 @@ __device__ __forceinline__ float gamma_lp_a(float a) {
   return 2.0f * logf(0.2f) + logf(a) - 0.2f * a;
 }
 
+// Device-side SVI loop (include/pert_hip.h): a launch of iteration st.step is a no-op once
+// an earlier iteration has stopped the fit.  The flag is written by pert_adam of the stopping
+// iteration (a previous launch), so a plain load at kernel start sees it.
+__device__ __forceinline__ bool loop_stopped(const pert_state& st) {
+  if (st.loop_ctl == nullptr) return false;
+  const int s = *(volatile const int32_t*)st.loop_ctl;
+  return s >= 0 && s < st.step;
+}
+
 // ------------------------------------------------------------------------------------------
 // Enumerated pass (steps 2/3).  MODE: PERT_MODE_STEP / PERT_MODE_GRAD / PERT_MODE_DECODE.
 template <int P, int MODE>
 __global__ void __launch_bounds__(kBlock, 2) enum_kernel(pert_problem pr, pert_state st,
                                                        pert_adam_hparams hp) {
   constexpr bool kDecode = MODE == PERT_MODE_DECODE;
+  if (MODE == PERT_MODE_STEP && loop_stopped(st)) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int N = pr.N, K1 = pr.K1;
   const int n = blockIdx.x * kBlock + tid;
@@ -297,6 +306,7 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
   constexpr int ZF = P * 64;                 // floats of one P-plane run
   constexpr int SF = ZF + 64 + 32;           // stage: z, x, code (64 x u16)
   constexpr int kStores = kStep ? 3 * P : (kDecode ? 2 : P);   // VMEM stores per iteration
+  if (kStep && loop_stopped(st)) return;
   // one dynamic LDS array (16-B aligned base, cdna_hip_programming.md G17):
   //   [stage 0 | stage 1 | m | v (STEP)] [per-bin rho partials: LT] [per-bin rho, gcf: LT x (K1+1)]
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -489,6 +499,7 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
 // ------------------------------------------------------------------------------------------
 // Observed pass (step 1): cn, rep conditioned (pert_model.py:724-729).
 __global__ void __launch_bounds__(kBlock) obs_kernel(pert_problem pr, pert_state st) {
+  if (loop_stopped(st)) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int N = pr.N, K1 = pr.K1;
   const int n = blockIdx.x * kBlock + tid;
@@ -586,58 +597,52 @@ __global__ void __launch_bounds__(kBlock) obs_kernel(pert_problem pr, pert_state
 }
 
 // ------------------------------------------------------------------------------------------
-// Per-cell and per-bin reductions + priors of the non-enumerated sites.
-// Blocks [0, n_cblk) handle 256 cells each; blocks [n_cblk, n_cblk + n_lblk) 256 bins each.
-// Per-cell partials [n_bt][K1+1][N] folded by kFoldT bin tiles: one thread per (cell,
-// chunk of kFoldT tiles) with all its loads independent, so the whole workspace is in
-// flight at once (a small shard has few cells but many bin tiles; the per-cell loop of
-// finalize_kernel alone is a latency chain there).  Output [ceil(n_bt/kFoldT)][K1+1][N].
-constexpr int kFoldT = 8;
-__global__ void __launch_bounds__(kBlock) fold_cell_part_kernel(const float* __restrict__ in,
-                                                               float* __restrict__ out, int N, int n_bt,
-                                                               int K1p1) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int n = blockIdx.x * 64 + lane;
-  const int c = blockIdx.y * kWaves + w;
-  const int b0 = c * kFoldT;
-  if (n >= N || b0 >= n_bt) return;
-  const int nb = min(kFoldT, n_bt - b0);
-  for (int k = 0; k < K1p1; ++k) {
-    float v[kFoldT];
-#pragma unroll
-    for (int i = 0; i < kFoldT; ++i) v[i] = i < nb ? in[((size_t)(b0 + i) * K1p1 + k) * N + n] : 0.0f;
-    double acc = 0.0;
-#pragma unroll
-    for (int i = 0; i < kFoldT; ++i) acc += (double)v[i];
-    out[((size_t)c * K1p1 + k) * N + n] = (float)acc;
-  }
-}
-
-__global__ void __launch_bounds__(kBlock) finalize_kernel(pert_problem pr, pert_state st,
-                                                          int n_cblk, int n_bt, int n_ct,
-                                                          const float* __restrict__ cell_part) {
+// Per-cell and per-bin reductions + priors of the non-enumerated sites, one launch.
+// 1024-thread workgroups = 64 items (lanes) x 16 groups (waves).  Blocks [0, n_cblk) take
+// 64 cells each: group g sums the per-cell partials [n_bt][K1+1][N] of bin tiles g, g+16,
+// ... (independent loads, kFinU tiles in flight per thread), the 16 group sums are added in
+// fixed order through LDS, and wave 0 applies the priors.  Blocks [n_cblk, n_cblk+n_lblk)
+// take 64 bins each and sum bin_part [n_ct][L] the same way.  Every item is reduced in one
+// memory round trip, so the launch stays short when a small shard has many bin tiles.
+constexpr int kFinBlock = 1024;
+constexpr int kFinG = kFinBlock / 64;
+template <int K1T>
+__global__ void __launch_bounds__(kFinBlock) finalize_kernel(pert_problem pr, pert_state st,
+                                                             int n_cblk, int n_bt, int n_ct) {
+  constexpr int kFinU = K1T <= 5 ? 4 : 2;    // bin tiles in flight per thread
+  if (loop_stopped(st)) return;
   const int tid = threadIdx.x;
-  const int N = pr.N, K1 = pr.K1, L = pr.L, nl = pr.n_libs;
+  const int lane = tid & 63, grp = tid >> 6;
+  const int N = pr.N, K1 = (K1T == PERT_MAX_K1) ? pr.K1 : K1T, L = pr.L, nl = pr.n_libs;
   const pert_layout lay = st.lay;
   const bool step1 = pr.kind == PERT_KIND_STEP1;
-  __shared__ double s_red[kWaves];
+  __shared__ double s_g[kFinG][64];
 
-  constexpr int kFG = 8;                 // reduction groups per workgroup (32 items x 8 groups)
   if ((int)blockIdx.x >= n_cblk) {
     // ---- per-bin: d(-ELBO)/dz_rho   (rho ~ Beta(1,1) has zero log density, :574)
-    __shared__ double s_bacc[kFG][32];
-    const int lb = tid & 31, grp = tid >> 5;
-    const int l = (blockIdx.x - n_cblk) * 32 + lb;
+    const int l = (blockIdx.x - n_cblk) * 64 + lane;
+    const bool on = l < L && pr.kind != PERT_KIND_STEP3;
     double s = 0.0;
-    if (l < L && pr.kind != PERT_KIND_STEP3)
-      for (int ct = grp; ct < n_ct; ct += kFG) s += (double)st.bin_part[(size_t)ct * L + l];
-    s_bacc[grp][lb] = s;
+    if (on) {
+      const float* __restrict__ bp = st.bin_part;
+      for (int c0 = grp; c0 < n_ct; c0 += kFinG * kFinU) {
+        float v[kFinU];
+#pragma unroll
+        for (int u = 0; u < kFinU; ++u) {
+          const int ct = c0 + u * kFinG;
+          v[u] = ct < n_ct ? bp[(size_t)ct * L + l] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < kFinU; ++u) s += (double)v[u];
+      }
+    }
+    s_g[grp][lane] = s;
     __syncthreads();
     if (grp != 0 || l >= L) return;
     if (pr.kind == PERT_KIND_STEP3) { st.grad_shared[lay.off_rho + l] = 0.0; return; }
     double tot = 0.0;
 #pragma unroll
-    for (int gi = 0; gi < kFG; ++gi) tot += s_bacc[gi][lb];
+    for (int g = 0; g < kFinG; ++g) tot += s_g[g][lane];
     const float a_val = fexp(st.params[lay.off_a]);
     float dmask;
     clipped_sigmoid(st.params[lay.off_rho + l], &dmask);
@@ -646,12 +651,49 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(pert_problem pr, pert_
     return;
   }
 
-  // ---- per-cell: 32 cells per workgroup; 8 groups split the bin tiles, then LDS
-  __shared__ double s_acc[kFG][PERT_MAX_K1 + 1][32];
-  const int cl = tid & 31, grp = tid >> 5;
-  const int n = blockIdx.x * 32 + cl;
+  // ---- per-cell
+  const int n = blockIdx.x * 64 + lane;
   const bool in_range = n < N;
-  const bool valid = in_range && grp == 0;
+  double A[K1T + 1];
+#pragma unroll
+  for (int k = 0; k <= K1T; ++k) A[k] = 0.0;
+  if (in_range) {
+    const float* __restrict__ cp = st.cell_part;
+    const size_t tstride = (size_t)(K1 + 1) * N;
+    for (int b0 = grp; b0 < n_bt; b0 += kFinG * kFinU) {
+      float v[kFinU][K1T + 1];
+#pragma unroll
+      for (int u = 0; u < kFinU; ++u) {
+        const int bt = b0 + u * kFinG;
+#pragma unroll
+        for (int k = 0; k <= K1T; ++k)
+          v[u][k] = (bt < n_bt && k <= K1) ? cp[(size_t)bt * tstride + (size_t)k * N + n] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < kFinU; ++u)
+#pragma unroll
+        for (int k = 0; k <= K1T; ++k) A[k] += (double)v[u][k];
+    }
+  }
+  // fixed-order sum of the 16 groups, one state slot at a time (wave 0 keeps the totals)
+  double T[K1T + 1];
+#pragma unroll
+  for (int k = 0; k <= K1T; ++k) {
+    T[k] = 0.0;
+    if (k > K1) continue;
+    s_g[grp][lane] = A[k];
+    __syncthreads();
+    if (grp == 0) {
+      double t = 0.0;
+#pragma unroll
+      for (int g = 0; g < kFinG; ++g) t += s_g[g][lane];
+      T[k] = t;
+    }
+    __syncthreads();
+  }
+  if (grp != 0) return;
+
+  const bool valid = in_range;
   float lam = pr.lamb;
   if (step1) {
     float dml;
@@ -659,48 +701,29 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(pert_problem pr, pert_
   }
   const float c0 = (1.0f - lam) / lam;
   double lp = 0.0;
-  float dzbs[PERT_MAX_K1], dbm[PERT_MAX_K1];
+  float dzbs[K1T], dbm[K1T];
   int lib = 0;
 #pragma unroll
-  for (int k = 0; k < PERT_MAX_K1; ++k) { dzbs[k] = 0.0f; dbm[k] = 0.0f; }
-  {
-    double A[PERT_MAX_K1 + 1];
-#pragma unroll
-    for (int k = 0; k <= PERT_MAX_K1; ++k) A[k] = 0.0;
-    if (in_range) {
-#pragma unroll 4
-      for (int bt = grp; bt < n_bt; bt += kFG) {
-        const float* cp = cell_part + (size_t)bt * (K1 + 1) * N + n;
-#pragma unroll
-        for (int k = 0; k <= PERT_MAX_K1; ++k)
-          if (k <= K1) A[k] += (double)cp[(size_t)k * N];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k <= PERT_MAX_K1; ++k) s_acc[grp][k][cl] = A[k];
-  }
-  __syncthreads();
+  for (int k = 0; k < K1T; ++k) { dzbs[k] = 0.0f; dbm[k] = 0.0f; }
   if (valid) {
-    double A[PERT_MAX_K1], T = 0.0;
+    double Ak[K1T], Tt = 0.0;
 #pragma unroll
-    for (int k = 0; k < PERT_MAX_K1; ++k) A[k] = 0.0;
+    for (int k = 0; k < K1T; ++k) Ak[k] = 0.0;
 #pragma unroll
-    for (int w = 0; w < kFG; ++w) {
-#pragma unroll
-      for (int k = 0; k < PERT_MAX_K1; ++k)
-        if (k < K1) A[k] += s_acc[w][k][cl];
-      T += s_acc[w][K1][cl];
+    for (int k = 0; k <= K1T; ++k) {
+      if (k < K1) Ak[k] = T[k];
+      if (k == K1) Tt = T[k];
     }
     const float u = st.params[lay.off_u + n];
     float dtau_dz;
     const float tau = clipped_sigmoid(st.params[lay.off_tau + n], &dtau_dz);
     lib = pr.libs[n];
     // data terms: dE/du = c0 sum_l gD omega (intercept column of gcf is 1), dE/dbeta_k = u c0 sum gD omega g_k
-    float dU = c0 * (float)A[K1 - 1];
-    float dTau = (float)T;
-    float dB[PERT_MAX_K1];
+    float dU = c0 * (float)Ak[K1 - 1];
+    float dTau = (float)Tt;
+    float dB[K1T];
 #pragma unroll
-    for (int k = 0; k < PERT_MAX_K1; ++k) dB[k] = (k < K1) ? u * c0 * (float)A[k] : 0.0f;
+    for (int k = 0; k < K1T; ++k) dB[k] = (k < K1) ? u * c0 * (float)Ak[k] : 0.0f;
 
     // u ~ Normal(mu, mu/10), mu = mean(x) / ((1 + tau) ploidy)   (:597-600)
     const float mu = pr.mean_reads[n] / ((1.0f + tau) * pr.ploidy[n]);
@@ -713,7 +736,7 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(pert_problem pr, pert_
 
     // betas ~ Normal(beta_means[lib], beta_stds[lib]).to_event(1)   (:603)
 #pragma unroll
-    for (int k = 0; k < PERT_MAX_K1; ++k) {
+    for (int k = 0; k < K1T; ++k) {
       if (k >= K1) continue;
       const float bsd = fexp(st.params[lay.off_bstds + lib * K1 + k]);
       const float bmn = step1 ? st.params[lay.off_bmeans + lib * K1 + k] : pr.beta_means[lib * K1 + k];
@@ -733,42 +756,30 @@ __global__ void __launch_bounds__(kBlock) finalize_kernel(pert_problem pr, pert_
     float* gc = st.grad_cell - lay.n_shared;
     gc[lay.off_u + n] = -dU;
 #pragma unroll
-    for (int k = 0; k < PERT_MAX_K1; ++k)
+    for (int k = 0; k < K1T; ++k)
       if (k < K1) gc[lay.off_beta + k * N + n] = -dB[k];
     gc[lay.off_tau + n] = -dTau * dtau_dz;
   }
   // per-library sums for beta_stds (and beta_means in step 1), plus the prior log densities:
-  // every slot reduced by wave shuffles, one LDS round, fixed order
+  // wave 0 holds every value, one wave reduction per slot, fixed order
   const int nslot = 2 * nl * K1 + 1;
   double* out = st.cellblk_part + (size_t)blockIdx.x * nslot;
-  __shared__ double s_fs[kWaves][64];
-  const int lane = tid & 63, wave = tid >> 6;
-  for (int s0 = 0; s0 < nslot; s0 += 64) {
-    for (int sl = s0; sl < min(nslot, s0 + 64); ++sl) {
-      double val;
-      if (sl < 2 * nl * K1) {
-        const int half = sl / (nl * K1), r = sl - half * nl * K1;
-        const int li = r / K1, k = r - li * K1;
-        const bool mine = valid && lib == li && (half == 0 || step1);
-        float fv = 0.0f;
+  for (int sl = 0; sl < nslot; ++sl) {
+    double val;
+    if (sl < 2 * nl * K1) {
+      const int half = sl / (nl * K1), r = sl - half * nl * K1;
+      const int li = r / K1, k = r - li * K1;
+      const bool mine = valid && lib == li && (half == 0 || step1);
+      float fv = 0.0f;
 #pragma unroll
-        for (int kk = 0; kk < PERT_MAX_K1; ++kk)
-          if (kk == k) fv = half == 0 ? dzbs[kk] : dbm[kk];
-        val = mine ? (double)fv : 0.0;
-      } else {
-        val = lp;
-      }
-      val = wave_sum_d(val);
-      if (lane == 0) s_fs[wave][sl - s0] = val;
+      for (int kk = 0; kk < K1T; ++kk)
+        if (kk == k) fv = half == 0 ? dzbs[kk] : dbm[kk];
+      val = mine ? (double)fv : 0.0;
+    } else {
+      val = lp;
     }
-    __syncthreads();
-    if (tid < min(nslot, s0 + 64) - s0) {
-      double t = 0.0;
-#pragma unroll
-      for (int w = 0; w < kWaves; ++w) t += s_fs[w][tid];
-      out[s0 + tid] = t;
-    }
-    __syncthreads();
+    val = wave_sum_d(val);
+    if (lane == 0) out[sl] = val;
   }
 }
 
@@ -788,6 +799,7 @@ __device__ __forceinline__ double block_sum_d1024(double v, double* sm) {
 
 __global__ void __launch_bounds__(kScalarBlock) scalar_kernel(pert_problem pr, pert_state st, int n_blk,
                                                               int n_cblk) {
+  if (loop_stopped(st)) return;
   const int tid = threadIdx.x;
   const int K1 = pr.K1, nl = pr.n_libs;
   const pert_layout lay = st.lay;
@@ -888,11 +900,49 @@ __global__ void __launch_bounds__(kScalarBlock) scalar_kernel(pert_problem pr, p
   st.grad_shared[lay.n_shared] = -elbo;                     // local loss (host adds constants)
 }
 
+// Loss of iteration st.step and the reference's stopping rule, evaluated by one thread after
+// the all-reduce (pert_model.py:742-758 / :800-816 / :867-883):
+//   losses.append(loss)
+//   if i >= min_iter: stop if |max(losses[-10:-1]) - min(losses[-10:-1])| / |losses[0] - losses[-1]| < rel_tol
+//   if isnan(loss): stop
+// in fp64 on the same values the host would see, so the stopping iteration is the host's.
+// (The reference raises on an empty window (min_iter = 0 at i = 0) or a zero denominator;
+// here those iterations simply do not stop.)
+__device__ void loop_record(const pert_state& st) {
+  const int t = st.step;
+  const double loss = st.grad_shared[st.lay.n_shared] - st.loss_const -
+                      (st.loss_offset != nullptr ? st.loss_offset[t] : 0.0);
+  double* rec = st.loop_rec;
+  int reason = 0;
+  if (t >= st.min_iter) {
+    const int lo = t - 9 > 0 ? t - 9 : 0;
+    if (t - 1 >= lo) {
+      double mx = rec[2 * lo], mn = mx;
+      for (int j = lo + 1; j <= t - 1; ++j) {
+        const double v = rec[2 * j];
+        mx = v > mx ? v : mx;
+        mn = v < mn ? v : mn;
+      }
+      const double diff = fabs(mx - mn) / fabs(rec[0] - loss);
+      if (diff < st.rel_tol) reason = 1;
+    }
+  }
+  if (reason == 0 && loss != loss) reason = 2;
+  rec[2 * t] = loss;
+  rec[2 * t + 1] = reason ? (double)t : -1.0;
+  if (reason) {
+    st.loop_ctl[1] = reason;
+    st.loop_ctl[0] = t;
+  }
+}
+
 // Adam on the packed params (torch.optim.Adam, pyro.optim.Adam wrapper; one state per param).
 __global__ void __launch_bounds__(kBlock) adam_kernel(pert_problem pr, pert_state st,
                                                       pert_adam_hparams hp) {
+  if (loop_stopped(st)) return;
   const int i = blockIdx.x * kBlock + threadIdx.x;
   const pert_layout lay = st.lay;
+  if (st.loop_ctl != nullptr && i == 0) loop_record(st);
   if (i >= lay.n_params) return;
   const int kind = pr.kind;
   bool active = true;
@@ -944,6 +994,12 @@ size_t dma_lds_bytes(int P, int mode, const pert_state& st, const pert_problem& 
 
 // cells per tile of the enumerated pass: 64 for the LDS-DMA kernel (variant 0), 256 otherwise
 int enum_cell_tile(const pert_state* st) { return st->variant == 0 ? 64 : kBlock; }
+// cell tiles launched: only tiles holding at least one real cell (the padding of ldn up to a
+// multiple of 256 is never visited by the 64-cell LDS-DMA tiles)
+int enum_cell_tiles(const pert_problem* pr, const pert_state* st) {
+  const int ct = enum_cell_tile(st);
+  return st->variant == 0 ? (pr->N + ct - 1) / ct : pr->ldn / ct;
+}
 
 template <int MODE>
 int launch_enum_mode(int P, dim3 grid, const pert_problem& pr, const pert_state& st,
@@ -965,6 +1021,32 @@ int launch_enum_mode(int P, dim3 grid, const pert_problem& pr, const pert_state&
     default: return PERT_E_UNSUPPORTED_P;
   }
   return hip_status(hipGetLastError());
+}
+
+// Resident one-wave workgroups per CU of the STEP-mode LDS-DMA pass at tile length lt.
+template <int P>
+int dma_step_occupancy(const pert_problem& pr, int lt) {
+  pert_state tmp{};
+  tmp.bins_per_tile = lt;
+  const size_t lds = dma_lds_bytes(P, PERT_MODE_STEP, tmp, pr);
+  int nb = 0;
+  hipError_t e;
+  if (pr.K1 == 5)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, enum_dma_kernel<P, PERT_MODE_STEP, 5>, 64, lds);
+  else
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, enum_dma_kernel<P, PERT_MODE_STEP, PERT_MAX_K1>, 64, lds);
+  return e == hipSuccess ? nb : 0;
+}
+
+int step_occupancy(const pert_problem& pr, int lt) {
+  switch (pr.P) {
+#define PERT_CASE(PP) case PP: return dma_step_occupancy<PP>(pr, lt);
+    PERT_CASE(2) PERT_CASE(3) PERT_CASE(4) PERT_CASE(5) PERT_CASE(6) PERT_CASE(7) PERT_CASE(8)
+    PERT_CASE(9) PERT_CASE(10) PERT_CASE(11) PERT_CASE(12) PERT_CASE(13) PERT_CASE(14)
+    PERT_CASE(15) PERT_CASE(16)
+#undef PERT_CASE
+    default: return 0;
+  }
 }
 
 template <int P>
@@ -1015,11 +1097,40 @@ int pert_workspace_sizes(int32_t kind, int32_t L, int32_t N, int32_t K1, int32_t
   const int lt = tile_bins(&tmp);
   const int64_t ldn = (N + kBlock - 1) / kBlock * kBlock;
   const int64_t n_bt = (L + lt - 1) / lt, n_ct = ldn / 64;     // sized for the 64-cell tiles
-  const int64_t n_fold = n_bt > kFoldMin ? (n_bt + kFoldT - 1) / kFoldT : 0;   // folded copy (finalize)
-  if (n_cell_part) *n_cell_part = (n_bt + n_fold) * (K1 + 1) * (int64_t)N;
+  if (n_cell_part) *n_cell_part = n_bt * (K1 + 1) * (int64_t)N;
   if (n_bin_part) *n_bin_part = n_ct * (int64_t)L;
   if (n_blk_part) *n_blk_part = n_bt * n_ct * kBlkSlots;
-  if (n_cellblk_part) *n_cellblk_part = ((N + 31) / 32) * (2 * (int64_t)n_libs * K1 + 1);
+  if (n_cellblk_part) *n_cellblk_part = ((N + 63) / 64) * (2 * (int64_t)n_libs * K1 + 1);
+  return PERT_OK;
+}
+
+int pert_auto_bins_per_tile(const pert_problem* prob, int32_t variant, int32_t* out) {
+  if (!prob || !out || prob->L <= 0 || prob->ldn <= 0 || prob->P < PERT_MIN_P || prob->P > PERT_MAX_P ||
+      prob->K1 < 1 || prob->K1 > PERT_MAX_K1)
+    return PERT_E_ARG;
+  *out = kDefaultLT;
+  if (variant != 0 || prob->kind == PERT_KIND_STEP1) return PERT_OK;
+  int dev = 0, ncu = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return hip_status(e);
+  // Each resident wave runs one tile (a prologue of about kTilePrologue bins plus lt bins);
+  // the pass takes ceil(tiles / slots) such rounds.  Pick the lt with the least predicted
+  // time, the longer tile on a tie.
+  constexpr int kTilePrologue = 2;
+  const long n_ct = (prob->N + 63) / 64;
+  long best = -1;
+  int best_lt = kDefaultLT;
+  for (int lt = kMaxLT; lt >= 8; --lt) {
+    const int occ = step_occupancy(*prob, lt);
+    if (occ <= 0) continue;
+    const long slots = (long)ncu * occ;
+    const long tiles = n_ct * ((prob->L + lt - 1) / lt);
+    const long rounds = (tiles + slots - 1) / slots;
+    const long cost = rounds * (lt + kTilePrologue);
+    if (best < 0 || cost < best) { best = cost; best_lt = lt; }
+  }
+  *out = best_lt;
   return PERT_OK;
 }
 
@@ -1037,8 +1148,7 @@ int pert_enum_pass(const pert_problem* prob, pert_state* st, const pert_adam_hpa
     return PERT_E_ARG;
   pert_state s2 = *st;
   s2.bins_per_tile = tile_bins(st);
-  const int ct = enum_cell_tile(st);
-  const dim3 grid(prob->ldn / ct, (prob->L + s2.bins_per_tile - 1) / s2.bins_per_tile);
+  const dim3 grid(enum_cell_tiles(prob, st), (prob->L + s2.bins_per_tile - 1) / s2.bins_per_tile);
   switch (mode) {
     case PERT_MODE_STEP: return launch_enum_mode<PERT_MODE_STEP>(prob->P, grid, *prob, s2, *hp, stream);
     case PERT_MODE_GRAD: return launch_enum_mode<PERT_MODE_GRAD>(prob->P, grid, *prob, s2, *hp, stream);
@@ -1062,24 +1172,16 @@ int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream) 
   pert_state s2 = *st;
   s2.bins_per_tile = tile_bins(st);
   const int lt = s2.bins_per_tile;
-  const int ct = prob->kind == PERT_KIND_STEP1 ? kBlock : enum_cell_tile(st);
-  const int n_ct = prob->ldn / ct;
+  const int n_ct = prob->kind == PERT_KIND_STEP1 ? prob->ldn / kBlock : enum_cell_tiles(prob, st);
   const int n_bt = (prob->L + lt - 1) / lt;
-  const int n_lblk = (prob->L + 31) / 32;
-  const int n_cblk = (prob->N + 31) / 32;
-  const float* cp = s2.cell_part;
-  int n_bt_f = n_bt;
-  if (n_bt > kFoldMin) {
-    n_bt_f = (n_bt + kFoldT - 1) / kFoldT;
-    float* folded = s2.cell_part + (size_t)n_bt * (prob->K1 + 1) * prob->N;
-    hipLaunchKernelGGL(fold_cell_part_kernel, dim3((prob->N + 63) / 64, (n_bt_f + kWaves - 1) / kWaves),
-                       dim3(kBlock), 0, stream, s2.cell_part, folded, prob->N, n_bt, prob->K1 + 1);
-    hipError_t e0 = hipGetLastError();
-    if (e0 != hipSuccess) return hip_status(e0);
-    cp = folded;
-  }
-  hipLaunchKernelGGL(finalize_kernel, dim3(n_cblk + n_lblk), dim3(kBlock), 0, stream, *prob, s2, n_cblk,
-                     n_bt_f, n_ct, cp);
+  const int n_lblk = (prob->L + 63) / 64;
+  const int n_cblk = (prob->N + 63) / 64;
+  if (prob->K1 == 5)
+    hipLaunchKernelGGL(finalize_kernel<5>, dim3(n_cblk + n_lblk), dim3(kFinBlock), 0, stream, *prob, s2, n_cblk,
+                       n_bt, n_ct);
+  else
+    hipLaunchKernelGGL(finalize_kernel<PERT_MAX_K1>, dim3(n_cblk + n_lblk), dim3(kFinBlock), 0, stream, *prob, s2,
+                       n_cblk, n_bt, n_ct);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_status(e);
   if (2 * prob->n_libs * prob->K1 + 1 > 64) return PERT_E_ARG;       // scalar_kernel's slot table

@@ -154,6 +154,13 @@ class CanonicalPiBlock:
         lp.backward()
         return float(lp.detach()), (-z.grad).numpy().astype(F32)             # loss gradient
 
+    def trajectory(self, t0: int, n: int) -> np.ndarray:
+        """log pi~ of steps t0 .. t0+n-1 (the values ``step`` would return), without
+        advancing this block: the per-step loss term of a device-side SVI loop."""
+        blk = CanonicalPiBlock(self.P, self.lr, (self.b1, self.b2), self.eps)
+        blk.z, blk.m, blk.v = self.z.copy(), self.m.copy(), self.v.copy()
+        return np.array([blk.step(t0 + i) for i in range(n)], dtype=np.float64)
+
     def step(self, t: int) -> float:
         lp, g = self.logp_and_grad()
         self.m = (self.b1 * self.m + (1 - self.b1) * g).astype(F32)
@@ -168,21 +175,6 @@ class CanonicalPiBlock:
 # --------------------------------------------------------------------------- shard
 def _ptr(t: Optional[torch.Tensor]) -> int:
     return 0 if t is None else int(t.data_ptr())
-
-
-def auto_bins_per_tile(kind: int, L: int, ldn: int, variant: int = 0, n_cu: int = 256) -> int:
-    """Bins per workgroup tile of the LDS-DMA enumerated pass: the longest of 64/32/16/8
-    that still gives >= 3 one-wave workgroups per wave slot of the chip (256 CUs x 8),
-    so long tiles amortise the per-tile prologue on big shards and short tiles keep the
-    chip full on small ones (strong-scaling shards)."""
-    if kind == nat.KIND_STEP1 or variant != 0:
-        return 32
-    slots = n_cu * 8
-    n_ct = ldn // 64
-    for lt in (64, 32, 16):
-        if n_ct * (-(-L // lt)) >= 3 * slots:
-            return lt
-    return 8
 
 
 class PertShard:
@@ -281,14 +273,6 @@ class PertShard:
         self.cn_out = torch.zeros((L, ldn), dtype=torch.uint8, device=dev)
         self.rep_out = torch.zeros((L, ldn), dtype=torch.uint8, device=dev)
 
-        if bins_per_tile <= 0:
-            bins_per_tile = auto_bins_per_tile(self.kind, L, ldn, variant)
-        ncp, nbp, nblk, ncb = nat.workspace_sizes(self.kind, L, N, self.K1, self.n_libs, bins_per_tile)
-        self.cell_part = torch.zeros(ncp, **f32)
-        self.bin_part = torch.zeros(nbp, **f32)
-        self.blk_part = torch.zeros(nblk, dtype=torch.float64, device=dev)
-        self.cellblk_part = torch.zeros(ncb, dtype=torch.float64, device=dev)
-        self.bins_per_tile = int(bins_per_tile)
         self.pass_events = None      # list -> (start, end) HIP events around every pass
 
         # ---- constants of the loss (added on the host, summed over ranks once)
@@ -315,6 +299,15 @@ class PertShard:
             log1m_lam=(math.log1p(-lam_f) if self.kind != nat.KIND_STEP1 else 0.0),
             sum_reads=self.sum_reads, a_fixed=float(a_fixed) if a_fixed is not None else 0.0,
             beta_means=_ptr(self.beta_means_t), rho_fixed=_ptr(self.rho_fixed_t))
+        if bins_per_tile <= 0:
+            with self._dev():
+                bins_per_tile = nat.auto_bins_per_tile(self._prob, variant)
+        ncp, nbp, nblk, ncb = nat.workspace_sizes(self.kind, L, N, self.K1, self.n_libs, bins_per_tile)
+        self.cell_part = torch.zeros(ncp, **f32)
+        self.bin_part = torch.zeros(nbp, **f32)
+        self.blk_part = torch.zeros(nblk, dtype=torch.float64, device=dev)
+        self.cellblk_part = torch.zeros(ncb, dtype=torch.float64, device=dev)
+        self.bins_per_tile = int(bins_per_tile)
         self._state = nat.PertState(
             lay=lay, params=_ptr(self.params), adam_m=_ptr(self.adam_m), adam_v=_ptr(self.adam_v),
             grad_shared=_ptr(self.grad_shared), grad_cell=_ptr(self.grad_cell), z_pi=_ptr(self.z_pi),
@@ -443,7 +436,13 @@ class PertShard:
     def step_async(self):
         """One SVI step without reading the loss back (the loss stays on the device)."""
         self.t += 1
-        self._set_hparams(self.t)
+        self._launch_step(self.t)
+        if self.pi_block is not None:
+            self._pi_lp = self.pi_block.step(self.t)
+
+    def _launch_step(self, t: int):
+        """Queue the launch sequence of Adam step t (1-based) on the current stream."""
+        self._set_hparams(t)
         if self.pass_events is not None:
             ev0 = torch.cuda.Event(enable_timing=True)
             ev1 = torch.cuda.Event(enable_timing=True)
@@ -457,8 +456,64 @@ class PertShard:
         with self._dev():
             nat.check(self.lib.pert_adam(ctypes.byref(self._prob), ctypes.byref(self._state),
                                          ctypes.byref(self._hp), self._stream()), "pert_adam")
+
+    def run_svi(self, max_iter: int, min_iter: int, rel_tol: float, chunk: int = 8, depth: int = 2):
+        """The SVI loop of pert_model.py:742-758 (:800-816, :867-883) without a per-step host
+        synchronisation.  Every iteration's loss is recorded on the device and the reference's
+        stopping rule (rel-tol plateau after min_iter, NaN) is evaluated there
+        (include/pert_hip.h, loop_ctl); launches of iterations after the stopping one are
+        no-ops.  The host queues iterations ahead, copies the loss records back every
+        ``chunk`` iterations and stops queueing once a copied record shows the stop (it is
+        at most ``chunk * depth`` iterations ahead).  Returns (losses, reason) with
+        reason 0 = max_iter reached, 1 = converged, 2 = NaN loss; the fit state is the one
+        after the last recorded iteration, exactly as if the loop had run on the host."""
+        n = int(max_iter)
+        if n <= 0:
+            return [], 0
+        dev = self.device
+        ctl = torch.tensor([-1, 0], dtype=torch.int32, device=dev)
+        rec = torch.zeros((n, 2), dtype=torch.float64, device=dev)
+        host = torch.empty((n, 2), dtype=torch.float64, pin_memory=True)
+        offs = None
+        t0 = self.t
         if self.pi_block is not None:
-            self._pi_lp = self.pi_block.step(self.t)
+            lps = self.pi_block.trajectory(t0 + 1, n)
+            offs = torch.as_tensor(float(self.L * self.n_cells_total) * lps, dtype=torch.float64, device=dev)
+        st = self._state
+        st.loop_ctl, st.loop_rec, st.loss_offset = _ptr(ctl), _ptr(rec), _ptr(offs)
+        st.loss_const, st.rel_tol, st.min_iter = float(self.const_total), float(rel_tol), int(min_iter)
+        launched = 0
+        pending = []
+        try:
+            for i in range(n):
+                st.step = i
+                self._launch_step(t0 + i + 1)
+                launched += 1
+                if (i + 1) % chunk == 0 or i == n - 1:
+                    j0 = (i // chunk) * chunk
+                    host[j0:i + 1].copy_(rec[j0:i + 1], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    pending.append((j0, i + 1, ev))
+                    stop_seen = False
+                    while len(pending) > depth:
+                        a, b, e = pending.pop(0)
+                        e.synchronize()
+                        stop_seen = stop_seen or bool((host[a:b, 1] >= 0).any())
+                    if stop_seen:
+                        break
+            c = ctl.cpu()                      # waits for every queued launch and copy
+        finally:
+            st.loop_ctl = st.loop_rec = st.loss_offset = None
+            st.step = 0
+        stop_at, reason = int(c[0]), int(c[1])
+        n_done = stop_at + 1 if stop_at >= 0 else launched
+        losses = host[:n_done, 0].tolist()
+        self.t = t0 + n_done
+        if self.pi_block is not None:
+            for k in range(n_done):
+                self._pi_lp = self.pi_block.step(t0 + 1 + k)
+        return losses, (reason if stop_at >= 0 else 0)
 
     def device_loss(self) -> float:
         """Loss of the last step: -(ELBO) with the host constants (pert_model.py:743 return value)."""

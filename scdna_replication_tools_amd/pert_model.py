@@ -129,20 +129,24 @@ class pert_infer_scRT():
 
     # ------------------------------------------------------------------ fits
     def _svi(self, shard: PertShard, max_iter: int, min_iter: int, label: str) -> List[float]:
-        """The SVI loop of pert_model.py:742-758 (also :800-816, :867-883)."""
-        losses: List[float] = []
+        """The SVI loop of pert_model.py:742-758 (also :800-816, :867-883).  The loss
+        record and the stopping rule run on the device (PertShard.run_svi), so the host
+        queues iterations without a per-step synchronisation; the losses, log lines and
+        stopping iteration are the ones the host loop below would produce:
+
+            for i in range(max_iter):
+                losses.append(svi.step(...))
+                if i >= min_iter and plateau(losses) < rel_tol: break
+                if isnan(losses[-1]): break
+        """
         t0 = time.perf_counter()
-        for i in range(max_iter):
-            loss = shard.step()
-            losses.append(loss)
+        losses, reason = shard.run_svi(max_iter, min_iter, self.rel_tol)
+        for i, loss in enumerate(losses):
             log.info('step: {}, loss: {}'.format(i, loss))
-            if _converged(losses, i, min_iter, self.rel_tol):
-                print('ELBO converged at iteration ' + str(i))
-                break
-            if np.isnan(loss):
-                print('ELBO is NaN at iteration ' + str(i))
-                break
-        torch.cuda.synchronize(self.device)
+        if reason == 1:
+            print('ELBO converged at iteration ' + str(len(losses) - 1))
+        elif reason == 2:
+            print('ELBO is NaN at iteration ' + str(len(losses) - 1))
         self.timings[label] = time.perf_counter() - t0
         self.iters[label] = len(losses)
         return losses

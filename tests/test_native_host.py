@@ -43,6 +43,9 @@ def test_struct_layout_matches_header(nat):
     assert ctypes.sizeof(nat.PertLayout) == 10 * 4
     assert nat.PertProblem.reads.offset == 9 * 4 + 4     # 9 int32 + padding to 8
     assert nat.PertState.params.offset == 40
+    # 15 pointers, LT and variant, then the device-loop block
+    assert nat.PertState.loop_ctl.offset == 40 + 15 * 8 + 2 * 4
+    assert ctypes.sizeof(nat.PertState) == nat.PertState.loop_ctl.offset + 3 * 8 + 2 * 8 + 2 * 4
 
 
 def test_layout_and_workspace(nat):
@@ -51,7 +54,7 @@ def test_layout_and_workspace(nat):
     assert lay.n_shared == 100 + 2 + 2 * 2 * 5
     assert lay.off_tau + 37 == lay.n_params
     ncp, nbp, nblk, ncb = nat.workspace_sizes(2, 100, 37, 5, 2, 32)
-    assert ncp == 4 * 6 * 37 and nbp == (256 // 64) * 100 and ncb == ((37 + 31) // 32) * (2 * 2 * 5 + 1)
+    assert ncp == 4 * 6 * 37 and nbp == (256 // 64) * 100 and ncb == ((37 + 63) // 64) * (2 * 2 * 5 + 1)
     with pytest.raises(ValueError):
         nat.make_layout(0, 1, 5, 1)
 

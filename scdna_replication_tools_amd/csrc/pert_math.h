@@ -72,8 +72,8 @@ PERT_HD float stirling_rem(float rz) {
 // invx = 1/x (0 when x == 0).
 //   d >= 8: asymptotic series on both arguments in cancellation-free form
 //     (d - 1/2) log1p(x/d) + x log1p(d/x) + S(d+x) - S(d)
-//   d <  8: shift d by k = ceil(8 - d) <= 7 with the recurrences
-//     lgamma(y) = lgamma(y + k) - log prod_{i<k} (y + i),  digamma(y) = digamma(y + k) - sum 1/(y + i).
+//   d <  8: shift d by 7 with the recurrences (nb_shift7)
+//     lgamma(y) = lgamma(y + 7) - log prod_{i<7} (y + i),  digamma(y) = digamma(y + 7) - sum 1/(y + i).
 PERT_HD void nb_lgdiff_asym(float d, float x, float invx, float& lam, float& psi) {
   // d >= 8 (no branches)
   const float r = frcp(d);
@@ -104,22 +104,43 @@ PERT_HD void nb_lgdiff_asym_hoisted(float d, float r, float x, float ldxc, float
         + 0.00833333333333333333f * (rz4 - r4) - 0.00396825396825396825f * (rz4 * rz2 - r4 * r2);
 }
 
+// 1 <= d < 8: shift by exactly 7 (d + 7 >= 8 for every d >= 1, so no per-lane shift count)
+// with the products A = prod_{i<7} (d+i), B = prod_{i<7} (d+x+i) and their d-derivatives
+// carried along (one fma + one mul per factor, no per-factor reciprocal):
+//   lgamma(d+x) - lgamma(d) = [lgamma(d+7+x) - lgamma(d+7)] - log(B / A)
+//   psi(d+x) - psi(d)       = [psi(d+7+x) - psi(d+7)] - B'/B + A'/A
+// The factors go in two groups (i < 4, i >= 4), each ratio B_g / A_g <= (1 + x)^4, so
+// nothing overflows for any count x < 4e9, and x = 0 gives exactly zero corrections.
+PERT_HD void nb_shift7(float d, float x, float& corr_l, float& corr_p) {
+  float A[2] = {1.0f, 1.0f}, Ap[2] = {0.0f, 0.0f}, B[2] = {1.0f, 1.0f}, Bp[2] = {0.0f, 0.0f};
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int g = i < 4 ? 0 : 1;
+    const float a = d + (float)i;
+    const float b = a + x;
+    Ap[g] = Ap[g] * a + A[g];
+    A[g] *= a;
+    Bp[g] = Bp[g] * b + B[g];
+    B[g] *= b;
+  }
+  corr_l = 0.0f;
+  corr_p = 0.0f;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const float rA = frcp(A[g]);
+    corr_l -= flog(B[g] * rA);
+    corr_p += Ap[g] * rA - Bp[g] * frcp(B[g]);
+  }
+  // x = 0: B = A, so both corrections are exactly 0 (fma contraction would leave ~1 ulp)
+  corr_l = x > 0.0f ? corr_l : 0.0f;
+  corr_p = x > 0.0f ? corr_p : 0.0f;
+}
+
 PERT_HD void nb_lgdiff(float d, float x, float invx, float& lam, float& psi) {
   float corr_l = 0.0f, corr_p = 0.0f;
   if (d < 8.0f) {
-    const float kf = ceilf(8.0f - d);
-    float num_a = 1.0f, num_b = 1.0f, den = 1.0f;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const bool on = (float)i < kf;
-      const float di = d + (float)i;
-      const float dxi = di + x;
-      if (i < 4) num_a *= on ? dxi : 1.0f; else num_b *= on ? dxi : 1.0f;
-      den *= on ? di : 1.0f;
-      corr_p += on ? x * frcp(di * dxi) : 0.0f;        // 1/di - 1/dxi
-    }
-    corr_l = -(flog(num_a) + flog(num_b) - flog(den));
-    d += kf;
+    nb_shift7(d, x, corr_l, corr_p);
+    d += 7.0f;
   }
   nb_lgdiff_asym(d, x, invx, lam, psi);
   lam += corr_l;

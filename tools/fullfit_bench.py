@@ -39,11 +39,13 @@ def main():
     sim = simulate(n_s=n, n_g=n, n_bins=nb, subdivide=sub, num_reads=1e6, seed=0)
     df_s, df_g = to_long_form(sim, n_libs=1)
     t_sim = time.perf_counter() - t0
+    print("simulated {} + {} cells x {} bins in {:.1f} s".format(n, n, sim.n_bins, t_sim), file=sys.stderr, flush=True)
     torch.zeros(1, device="cuda")
     m = pert_infer_scRT(df_s, df_g, input_col='reads', clone_col='clone_id', cn_prior_method=args.prior,
                         max_iter=args.max_iter, min_iter=args.min_iter, run_step3=not args.no_step3,
                         n_jobs=args.n_jobs)
     cn_s_out, supp_s, cn_g1_out, supp_g1 = m.run_pert_model()
+    print("fit done: {}".format(m.timings), file=sys.stderr, flush=True)
     acc_cn = float((cn_s_out["model_cn_state"] == cn_s_out["true_somatic_cn"]).mean())
     acc_rep = float((cn_s_out["model_rep_state"] == cn_s_out["true_rep"]).mean())
     tm = m.timings
@@ -53,6 +55,7 @@ def main():
            "fit_steps12_s": tm["total"] - sum(tm.get(k, 0.0) for k in ("prep_step3", "step3", "decode_package_g")),
            "acc_cn": acc_cn, "acc_rep": acc_rep}
     if args.cpu_sample_cells > 0:
+        print("timing the CPU oracle on {} cells".format(args.cpu_sample_cells), file=sys.stderr, flush=True)
         rec["cpu_extrapolated"] = cpu_extrapolation(sim, m.iters, args.cpu_sample_cells)
         fit12 = rec["cpu_extrapolated"]["step1_s"] + rec["cpu_extrapolated"]["step2_s"]
         rec["speedup_fit_steps12_vs_cpu"] = fit12 / rec["fit_steps12_s"]

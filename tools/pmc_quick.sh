@@ -19,9 +19,12 @@ cd "$R" && python3 - "$OUT" <<'PY'
 import csv, glob, sys, collections
 acc = collections.defaultdict(list)
 for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(f)):
-        acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
-# one value per dispatch per counter (summed over dimensions by rocprofv3 csv rows)
+        per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
+    for cs in per.values():
+        for c, v in cs.items():
+            acc[c].append(v)
 for k, v in sorted(acc.items()):
     print("{:28s} {:.4g}".format(k, sum(v) / max(1, len(v))))
 PY

@@ -4,8 +4,9 @@ PERT level only.
 ``scRT(cn_s, cn_g1, ...).infer(level='pert')`` (or 'pyro') computes the consensus clone
 profiles of ``assign_col``, assigns every S-phase cell to its best-correlated clone
 (assign_s_to_clones.py:49-79, vectorised) and runs ``pert_infer_scRT`` on the GPU.
-The deterministic 'cell' / 'clone' / 'bulk' levels and the KMeans clustering used when
-``clone_col`` is None are outside this build's scope and raise.
+When ``clone_col`` is None the G1/2 cells are first clustered by KMeans + BIC
+(cncluster.kmeans_cluster, infer_scRT.py:129-138).  The deterministic 'cell' / 'clone' /
+'bulk' levels are outside this build's scope and raise.
 """
 from __future__ import annotations
 
@@ -13,6 +14,7 @@ import numpy as np
 import pandas as pd
 
 from . import prep
+from .cncluster import kmeans_cluster
 from .pert_model import pert_infer_scRT
 
 
@@ -111,7 +113,19 @@ class scRT:
     def infer_pert_model(self):
         """infer_scRT.py:127-168."""
         if self.clone_col is None:
-            raise NotImplementedError("clone_col=None needs the KMeans clustering of cncluster.py (out of scope)")
+            # no clone labels: KMeans + BIC over the G1/2 cells' assign_col profiles (:129-138)
+            piv = prep.pivot_cells_by_loci(self.cn_g1, self.assign_col, self.cell_col, self.chr_col, self.start_col)
+            g1_mat = pd.DataFrame(piv.values, columns=pd.Index(piv.cells, name=self.cell_col),
+                                  index=pd.MultiIndex.from_arrays([piv.loci_chr, piv.loci_start],
+                                                                  names=[self.chr_col, self.start_col]))
+            clusters = kmeans_cluster(g1_mat, max_k=20, device=self.engine_kwargs.get("device"))
+            self.clusters = clusters
+            # pd.merge(cn_g1, clusters, on=cell_col) for an inner join on a complete cluster table
+            lut = pd.Series(clusters["cluster_id"].to_numpy(), index=clusters["cell_id"].to_numpy())
+            self.cn_g1 = self.cn_g1.assign(cluster_id=self.cn_g1[self.cell_col].map(lut))
+            self.cn_g1 = self.cn_g1[self.cn_g1["cluster_id"].notna()]
+            self.cn_g1["cluster_id"] = self.cn_g1["cluster_id"].astype(np.int64)
+            self.clone_col = 'cluster_id'
         self.clone_profiles = prep.consensus_clone_profiles(
             self.cn_g1, self.assign_col, clone_col=self.clone_col, cell_col=self.cell_col, chr_col=self.chr_col,
             start_col=self.start_col, cn_state_col=self.cn_state_col)

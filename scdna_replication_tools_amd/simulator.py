@@ -143,16 +143,27 @@ def simulate(n_s: int, n_g: Optional[int] = None, n_bins: Optional[int] = None, 
                          clone_g=clone_g, clone_cn=prof)
 
 
-def to_long_form(sim: SyntheticPERT, input_col: str = "reads", n_libs: int = 1):
+def to_long_form(sim: SyntheticPERT, input_col: str = "reads", n_libs: int = 1, copy_from: str = "state"):
     """Long-form DataFrames (one row per cell x bin) with the columns the
     reference entry points consume (``pert_infer_scRT``, pert_model.py:37-43) plus
-    the simulator's truth columns (pert_simulator.py:371-418)."""
+    the simulator's truth columns (pert_simulator.py:371-418).
+
+    ``copy`` (HMMcopy's copy-number estimate, the default ``assign_col``) is the true
+    state (``copy_from='state'``) or a noisy estimate from the reads: each cell's reads
+    scaled to its mean state (``copy_from='reads'``, what clustering needs)."""
     import pandas as pd
     L = sim.n_bins
     clone_names = np.array([chr(ord("A") + i) for i in range(sim.clone_cn.shape[1])])
 
     def frame(reads, cn, clone, prefix, rep=None, tau=None):
         n = reads.shape[1]
+        if copy_from == "reads":
+            r = reads.astype(np.float64)
+            copy = r / np.maximum(r.mean(0, keepdims=True), 1e-12) * cn.mean(0, keepdims=True)
+        elif copy_from == "state":
+            copy = cn.astype(np.float64)
+        else:
+            raise ValueError(copy_from)
         cells = np.array(["cell_{}_{}".format(prefix, i) for i in range(n)])
         d = {
             "cell_id": np.tile(cells, L),
@@ -163,7 +174,7 @@ def to_long_form(sim: SyntheticPERT, input_col: str = "reads", n_libs: int = 1):
             "library_id": np.tile(np.array(["LIB{}".format(i % n_libs) for i in range(n)]), L),
             "clone_id": np.tile(clone_names[clone], L),
             "state": cn.reshape(-1).astype(np.int64),
-            "copy": cn.reshape(-1).astype(np.float64),
+            "copy": copy.reshape(-1),
             input_col: reads.reshape(-1),
             "true_somatic_cn": cn.reshape(-1),
         }

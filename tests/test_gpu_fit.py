@@ -70,3 +70,32 @@ def test_pipeline_end_to_end():
     # step 3 (G1 cells under the S-phase model, rho and a frozen) returns valid states
     assert set(np.unique(cn_g1_out["model_rep_state"])) <= {0.0, 1.0}
     assert (cn_g1_out["model_cn_state"] == cn_g1_out["true_somatic_cn"]).mean() > 0.9
+
+
+def test_scrt_polyclonal_without_clone_labels():
+    """BASELINE configs[1] stand-in (polyclonal, unknown clones): scRT with clone_col=None
+    clusters the G1/2 cells (KMeans + BIC on the device), assigns S cells to the clusters and
+    fits PERT (infer_scRT.py:127-168)."""
+    import pandas as pd
+    from scdna_replication_tools_amd.infer_scRT import scRT
+    from scdna_replication_tools_amd.simulator import simulate, to_long_form
+    sim = simulate(n_s=45, n_g=45, n_bins=300, num_reads=183 * 300, seed=4)
+    df_s, df_g = to_long_form(sim, n_libs=1, copy_from="reads")
+    truth_g = df_g.drop_duplicates("cell_id").set_index("cell_id")["clone_id"]
+    m = scRT(df_s.drop(columns=["clone_id"]), df_g.drop(columns=["clone_id"]), clone_col=None,
+             cn_prior_method='g1_clones', max_iter=300, min_iter=50, max_iter_step1=200, max_iter_step3=100)
+    cn_s_out, supp_s, cn_g1_out, supp_g1 = m.infer(level='pert')
+    cl = m.clusters.set_index("cell_id")["cluster_id"]
+    t = pd.crosstab(cl.to_numpy(), truth_g.loc[cl.index].to_numpy())
+    assert t.shape == (3, 3) and ((t > 0).sum(1) == 1).all() and ((t > 0).sum(0) == 1).all()
+    # S cells go to the cluster whose consensus 'copy' profile they correlate with best
+    # (assign_s_to_clones); on 300 bins the replication signal misleads some of them, so the
+    # CN calls are checked on the S cells whose cluster is their true clone
+    to_clone = t.idxmax(axis=1)
+    right = cn_s_out["cluster_id"].map(to_clone) == cn_s_out["cell_id"].map(
+        df_s.drop_duplicates("cell_id").set_index("cell_id")["clone_id"])
+    assert right.mean() > 0.4
+    ok = cn_s_out[right]
+    acc_cn = (ok["model_cn_state"] == ok["true_somatic_cn"]).mean()
+    acc_rep = (cn_s_out["model_rep_state"] == cn_s_out["true_rep"]).mean()
+    assert acc_cn > 0.97 and acc_rep > 0.85, (acc_cn, acc_rep)

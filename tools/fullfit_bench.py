@@ -13,11 +13,15 @@ import sys
 import time
 
 import numpy as np
+import pandas as pd
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-CONFIGS = {"c1": (400, 271, 1), "c3": (2000, None, 1), "c4": (10000, None, 1), "c5": (2000, None, 25)}
+CONFIGS = {"c1": (400, 271, 1), "c2": (2000, None, 1), "c3": (2000, None, 1), "c4": (10000, None, 1),
+           "c5": (2000, None, 25)}
+# c2: BASELINE configs[1] stand-in (polyclonal sample, clones unknown): C3-sized synthetic data
+# through scRT(clone_col=None).infer('pert') -- KMeans + BIC clustering of the G1/2 cells first.
 
 
 def main():
@@ -37,14 +41,29 @@ def main():
     n, nb, sub = CONFIGS[args.config]
     t0 = time.perf_counter()
     sim = simulate(n_s=n, n_g=n, n_bins=nb, subdivide=sub, num_reads=1e6, seed=0)
-    df_s, df_g = to_long_form(sim, n_libs=1)
+    df_s, df_g = to_long_form(sim, n_libs=1, copy_from="reads" if args.config == "c2" else "state")
     t_sim = time.perf_counter() - t0
     print("simulated {} + {} cells x {} bins in {:.1f} s".format(n, n, sim.n_bins, t_sim), file=sys.stderr, flush=True)
     torch.zeros(1, device="cuda")
-    m = pert_infer_scRT(df_s, df_g, input_col='reads', clone_col='clone_id', cn_prior_method=args.prior,
-                        max_iter=args.max_iter, min_iter=args.min_iter, run_step3=not args.no_step3,
-                        n_jobs=args.n_jobs)
-    cn_s_out, supp_s, cn_g1_out, supp_g1 = m.run_pert_model()
+    if args.config == "c2":
+        from scdna_replication_tools_amd.infer_scRT import scRT
+        t0 = time.perf_counter()
+        sc = scRT(df_s.drop(columns=["clone_id"]), df_g.drop(columns=["clone_id"]), clone_col=None,
+                  cn_prior_method=args.prior, max_iter=args.max_iter, min_iter=args.min_iter,
+                  run_step3=not args.no_step3, n_jobs=args.n_jobs)
+        cn_s_out, supp_s, cn_g1_out, supp_g1 = sc.infer(level='pert')
+        m = sc.model
+        m.timings["cluster_assign"] = time.perf_counter() - t0 - m.timings["total"]
+        truth = df_g.drop_duplicates("cell_id").set_index("cell_id")["clone_id"]
+        cl = sc.clusters.set_index("cell_id")["cluster_id"]
+        ct = pd.crosstab(cl.to_numpy(), truth.loc[cl.index].to_numpy())
+        clusters_ok = bool(((ct > 0).sum(1) == 1).all() and ((ct > 0).sum(0) == 1).all())
+    else:
+        m = pert_infer_scRT(df_s, df_g, input_col='reads', clone_col='clone_id', cn_prior_method=args.prior,
+                            max_iter=args.max_iter, min_iter=args.min_iter, run_step3=not args.no_step3,
+                            n_jobs=args.n_jobs)
+        cn_s_out, supp_s, cn_g1_out, supp_g1 = m.run_pert_model()
+        clusters_ok = None
     print("fit done: {}".format(m.timings), file=sys.stderr, flush=True)
     acc_cn = float((cn_s_out["model_cn_state"] == cn_s_out["true_somatic_cn"]).mean())
     acc_rep = float((cn_s_out["model_rep_state"] == cn_s_out["true_rep"]).mean())
@@ -54,6 +73,9 @@ def main():
            "ms_per_step": {k: 1e3 * tm[k] / max(1, m.iters[k]) for k in m.iters},
            "fit_steps12_s": tm["total"] - sum(tm.get(k, 0.0) for k in ("prep_step3", "step3", "decode_package_g")),
            "acc_cn": acc_cn, "acc_rep": acc_rep}
+    if clusters_ok is not None:
+        rec["clusters_match_truth"] = clusters_ok
+        rec["n_clusters"] = int(sc.clusters["cluster_id"].nunique())
     if args.cpu_sample_cells > 0:
         print("timing the CPU oracle on {} cells".format(args.cpu_sample_cells), file=sys.stderr, flush=True)
         rec["cpu_extrapolated"] = cpu_extrapolation(sim, m.iters, args.cpu_sample_cells)

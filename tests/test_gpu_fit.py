@@ -70,6 +70,16 @@ def test_pipeline_end_to_end():
     # step 3 (G1 cells under the S-phase model, rho and a frozen) returns valid states
     assert set(np.unique(cn_g1_out["model_rep_state"])) <= {0.0, 1.0}
     assert (cn_g1_out["model_cn_state"] == cn_g1_out["true_somatic_cn"]).mean() > 0.9
+    # downstream consumer of the decode: cell-cycle phase calls (predict_cycle_phase.py:102-120)
+    import pandas as pd
+    from scdna_replication_tools_amd.predict_cycle_phase import predict_cycle_phase
+    cn = pd.concat([cn_s_out.assign(true_phase="S"), cn_g1_out.assign(true_phase="G")], ignore_index=True)
+    cn["rpm"] = cn["reads"] / cn.groupby("cell_id")["reads"].transform("sum") * 1e6
+    s_, g_, lq_ = predict_cycle_phase(cn)
+    calls = pd.concat([s_, g_, lq_]).drop_duplicates("cell_id").set_index("cell_id")
+    truth = calls["true_phase"]
+    assert (calls.loc[truth == "G", "PERT_phase"] == "G1/2").mean() > 0.9
+    assert (calls.loc[truth == "S", "PERT_phase"] == "S").mean() > 0.6
 
 
 def test_scrt_polyclonal_without_clone_labels():

@@ -49,7 +49,7 @@ def bytes_per_cellbin(P: int) -> int:
     return 4 + 2 + 24 * P
 
 
-def synth(n_total: int, subdivide: int, seed: int, device):
+def synth(n_total: int, subdivide: int, seed: int, device, num_reads: float = 1e6):
     """Seeded synthetic S-phase data on the GPU following pert_simulator.py:201-249."""
     from scdna_replication_tools_amd.simulator import clone_profiles, convert_rt_units, load_bins
     df = load_bins(subdivide=subdivide)
@@ -67,11 +67,11 @@ def synth(n_total: int, subdivide: int, seed: int, device):
     rep = (torch.rand(phi.shape, generator=g, device=device, dtype=torch.float64) < phi).double()
     omega = torch.exp(0.5 * torch.as_tensor(gc, device=device))[:, None]
     lam = 0.75
-    u = 1e6 / (1.5 * L * float(cn.mean()))
+    u = num_reads / (1.5 * L * float(cn.mean()))
     delta = (u * cn * (1 + rep) * omega * (1 - lam) / lam).clamp(min=1.0)
     rate = torch._standard_gamma(delta) * (lam / (1 - lam))
     raw = torch.poisson(rate, generator=g)
-    reads = torch.floor(raw / raw.sum(0, keepdim=True) * 1e6)
+    reads = torch.floor(raw / raw.sum(0, keepdim=True) * num_reads)
     return dict(gc=gc, reads=reads.float(), cn=cn.to(torch.int64), tau=tau.float(), clone_prof=prof, clone=clone)
 
 
@@ -113,6 +113,8 @@ def main():
     ap.add_argument("--bins-per-tile", type=int, default=0)
     ap.add_argument("--variant", type=int, default=0, help="enumerated-pass kernel: 0 LDS-DMA, 1 register")
     ap.add_argument("--cells", type=int, default=0, help="override the config's cell count (per job)")
+    ap.add_argument("--subdivide", type=int, default=0, help="override the config's bin subdivision")
+    ap.add_argument("--reads-per-cell", type=float, default=1e6, help="synthetic library size per cell")
     ap.add_argument("--cpu-cells", type=int, default=640)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -135,11 +137,14 @@ def main():
     from scdna_replication_tools_amd.sharding import cell_bounds, make_allreduce
 
     n_cells, subdiv, desc = CONFIGS[args.config]
+    if args.subdivide > 0:
+        subdiv = args.subdivide
+        desc = "synthetic {} cells x {} bins (--subdivide override of {})".format(n_cells, 5451 * subdiv, args.config)
     if args.cells > 0:
         n_cells = args.cells
-        desc = "synthetic {} cells x {} bins (--cells override of {})".format(n_cells, 5451 * subdiv, args.config)
+        desc = "synthetic {} cells x {} bins (override of {})".format(n_cells, 5451 * subdiv, args.config)
     n_total = n_cells * (world if args.scaling == "weak" else 1)
-    data = synth(n_total, subdiv, seed=0, device=device)
+    data = synth(n_total, subdiv, seed=0, device=device, num_reads=args.reads_per_cell)
     L = data["reads"].shape[0]
     n0, n1 = cell_bounds(n_total, world)[rank]
     reads = data["reads"][:, n0:n1].cpu().numpy()
@@ -207,7 +212,7 @@ def main():
                        "bins_per_tile": shard.bins_per_tile},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
-                         "kernel": ("enum_dma_kernel<13, STEP, 5>" if args.variant == 0 else "enum_kernel<13, STEP>"),
+                         "kernel": ("enum_dma_kernel<13, STEP, 5>" if args.variant != 1 else "enum_kernel<13, STEP>"),
                          "kernel_ms": kern_ms,
                          "bytes_per_cellbin": bpc},
             "loss_first": losses[0], "loss_last": losses[-1],

@@ -307,6 +307,7 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
   constexpr int SF = ZF + 64 + 32;           // stage: z, x, code (64 x u16)
   constexpr int kStores = kStep ? 3 * P : (kDecode ? 2 : P);   // VMEM stores per iteration
   if (kStep && loop_stopped(st)) return;
+  const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
   // one dynamic LDS array (16-B aligned base, cdna_hip_programming.md G17):
   //   [stage 0 | stage 1 | m | v (STEP)] [per-bin rho partials: LT] [per-bin rho, gcf: LT x (K1+1)]
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -375,8 +376,28 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
   if (l0 < l1) issue_stage(l0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
+  // variant 2 = diagnostic build of the same kernel: wave timeline stamps (s_memrealtime,
+  // 100 MHz) at entry, after the first stage landed and at exit, into the g_pi buffer
+  // (unused in STEP mode) -- tools/wave_timeline.py.
+  const bool stamps = kStep && st.variant == 2 && st.g_pi != nullptr;
+  unsigned long long* dbg = (unsigned long long*)st.g_pi + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4;
+  if (stamps && lane == 0) dbg[1] = __builtin_amdgcn_s_memrealtime();
+  // Issue priority falls with the wave's progress through its tile (3, 2, 1, 0 by quarters).
+  // Arbitration between ready waves of a SIMD is by priority, then age, so at equal priority
+  // the older of the two resident waves runs ahead and the younger finishes its tile alone,
+  // latency-bound (tools/wave_timeline.py: exits bimodal at 340 / 590 us on a one-round
+  // 1,250-cell launch).  Favouring the wave that is behind closes the gap (exit spread
+  // 340-590 -> 440-530 us; -3.4 % kernel at 1,250 cells, -0.9 % at 10 k).
+  const int nbt = l1 - l0;
+  __builtin_amdgcn_s_setprio(3);
   for (int l = l0; l < l1; ++l) {
     const int buf = (l - l0) & 1;
+    {
+      const int q4 = 4 * (l - l0);
+      if (q4 >= nbt && q4 - 4 < nbt) __builtin_amdgcn_s_setprio(2);
+      if (q4 >= 2 * nbt && q4 - 4 < 2 * nbt) __builtin_amdgcn_s_setprio(1);
+      if (q4 >= 3 * nbt && q4 - 4 < 3 * nbt) __builtin_amdgcn_s_setprio(0);
+    }
     // stage(l) was issued one iteration ago; only this wave's stores of bin l-1
     // (kStores, unconditional) may be younger than it
     if (l > l0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(kStores) : "memory");
@@ -473,6 +494,15 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (stamps && lane == 0) {
+    dbg[0] = t_entry;
+    dbg[2] = __builtin_amdgcn_s_memrealtime();
+    unsigned int hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    unsigned int xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    dbg[3] = ((unsigned long long)xcc << 32) | hw;
+  }
   if (kDecode) return;
   __syncthreads();
   if (!frozen) {
@@ -993,18 +1023,18 @@ size_t dma_lds_bytes(int P, int mode, const pert_state& st, const pert_problem& 
 }
 
 // cells per tile of the enumerated pass: 64 for the LDS-DMA kernel (variant 0), 256 otherwise
-int enum_cell_tile(const pert_state* st) { return st->variant == 0 ? 64 : kBlock; }
+int enum_cell_tile(const pert_state* st) { return st->variant != 1 ? 64 : kBlock; }
 // cell tiles launched: only tiles holding at least one real cell (the padding of ldn up to a
 // multiple of 256 is never visited by the 64-cell LDS-DMA tiles)
 int enum_cell_tiles(const pert_problem* pr, const pert_state* st) {
   const int ct = enum_cell_tile(st);
-  return st->variant == 0 ? (pr->N + ct - 1) / ct : pr->ldn / ct;
+  return st->variant != 1 ? (pr->N + ct - 1) / ct : pr->ldn / ct;
 }
 
 template <int MODE>
 int launch_enum_mode(int P, dim3 grid, const pert_problem& pr, const pert_state& st,
                      const pert_adam_hparams& hp, hipStream_t s) {
-  const bool dma = st.variant == 0;
+  const bool dma = st.variant != 1;
   switch (P) {
 #define PERT_CASE(PP)                                                                             \
   case PP:                                                                                        \
@@ -1109,7 +1139,7 @@ int pert_auto_bins_per_tile(const pert_problem* prob, int32_t variant, int32_t* 
       prob->K1 < 1 || prob->K1 > PERT_MAX_K1)
     return PERT_E_ARG;
   *out = kDefaultLT;
-  if (variant != 0 || prob->kind == PERT_KIND_STEP1) return PERT_OK;
+  if (variant == 1 || prob->kind == PERT_KIND_STEP1) return PERT_OK;
   int dev = 0, ncu = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);

@@ -1,0 +1,49 @@
+"""Wave timeline of the enumerated pass (diagnostic build, variant 2): per workgroup the
+s_memrealtime stamps (100 MHz) at entry, first-bin start and exit, plus the XCC / HW ids.
+Prints the launch span, entry / exit spreads and how many waves are resident over time.
+usage: python tools/wave_timeline.py CELLS [SUBDIVIDE]"""
+import os, sys
+import numpy as np
+import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench
+from scdna_replication_tools_amd.engine import EtaCodebook, PertShard, _ptr
+from scdna_replication_tools_amd.init import init_params
+
+cells = int(sys.argv[1]) if len(sys.argv) > 1 else 1250
+sub = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+dev = torch.device("cuda", 0)
+data = bench.synth(cells, sub, 0, dev, num_reads=1e6 * sub)
+reads = data["reads"].cpu().numpy(); states = data["cn"].cpu().numpy()
+eta = EtaCodebook.from_states(states, 1e6, 13)
+bm = np.zeros((1, 5)); bm[0, 3] = 0.5
+init = init_params(2, reads, np.zeros(cells, int), 1, 13, 4, ploidy=eta.argmax_states().mean(0),
+                   t_init=np.clip(data["tau"].cpu().numpy(), 0.05, 0.95), beta_means=bm, seed=0)
+sh = PertShard(2, reads, data["gc"], np.zeros(cells, int), 1, 13, 4, init, eta=eta, lamb=0.75, beta_means=bm,
+               device=dev, variant=int(os.environ.get("VARIANT", "2")))
+L = reads.shape[0]
+n_wg = (-(-cells // 64)) * (-(-L // sh.bins_per_tile))
+dbg = torch.zeros(n_wg * 4, dtype=torch.int64, device=dev)
+sh._state.g_pi = _ptr(dbg)
+for t in range(1, 8):
+    sh._launch_step(t)
+torch.cuda.synchronize()
+d = dbg.cpu().numpy().reshape(n_wg, 4)
+t0 = d[:, 0].min()
+ent, first, ex = (d[:, 0] - t0) / 100.0, (d[:, 1] - t0) / 100.0, (d[:, 2] - t0) / 100.0   # microseconds
+span = ex.max()
+dur = ex - ent
+print("cells {} bins {} LT {} workgroups {}: span {:.1f} us".format(cells, L, sh.bins_per_tile, n_wg, span))
+q = lambda a: " ".join("{:.1f}".format(v) for v in np.percentile(a, [0, 10, 50, 90, 100]))
+print("entry     pct 0/10/50/90/100: ", q(ent))
+print("first bin pct                :", q(first - ent))
+print("exit      pct                :", q(ex))
+print("wave dur  pct                :", q(dur))
+grid = np.linspace(0, span, 41)
+res = [int(((ent <= g) & (ex > g)).sum()) for g in grid]
+print("resident waves over time (41 samples):", res)
+xcc = (d[:, 3] >> 32).astype(int)
+for x in range(8):
+    m = xcc == x
+    if m.any():
+        print("xcc {} waves {} exit p50 {:.1f} p100 {:.1f} mean dur {:.1f}".format(x, m.sum(), np.median(ex[m]), ex[m].max(), dur[m].mean()))

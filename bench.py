@@ -111,6 +111,8 @@ def main():
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     ap.add_argument("--bins-per-tile", type=int, default=0)
+    ap.add_argument("--fit", default="step2", choices=["step1", "step2", "step3"],
+                    help="which SVI fit's step to time (the metric is step 2's)")
     ap.add_argument("--variant", type=int, default=0, help="enumerated-pass kernel: 0 LDS-DMA, 1 register")
     ap.add_argument("--cells", type=int, default=0, help="override the config's cell count (per job)")
     ap.add_argument("--subdivide", type=int, default=0, help="override the config's bin subdivision")
@@ -161,12 +163,28 @@ def main():
     bm[0, K - 1] = 0.5                                                # betas [0.5, 0] of the simulator
     t_init = np.clip(data["tau"][n0:n1].cpu().numpy(), 0.05, 0.95)
     ploidy = eta.argmax_states().mean(0)
-    init = init_params(2, reads, np.zeros(n1 - n0, int), 1, P, K, ploidy=ploidy, t_init=t_init,
-                       beta_means=bm, seed=0)
     allreduce = make_allreduce()
-    shard = PertShard(2, reads, data["gc"], np.zeros(n1 - n0, int), 1, P, K, init, eta=eta, lamb=0.75,
-                      beta_means=bm, device=device, is_root=(rank == 0), n_cells_total=n_total,
-                      allreduce=allreduce, bins_per_tile=args.bins_per_tile, variant=args.variant)
+    libs = np.zeros(n1 - n0, int)
+    common = dict(device=device, is_root=(rank == 0), allreduce=allreduce, bins_per_tile=args.bins_per_tile,
+                  variant=args.variant)
+    if args.fit == "step1":
+        # step 1 (pert_model.py:718-774): the same cells as G1/2 cells, doubled with rep 0 / 1
+        st2 = np.concatenate([states, states], 1)
+        rd2 = np.concatenate([reads, reads], 1)
+        rep2 = np.concatenate([np.zeros_like(states), np.ones_like(states)], 1)
+        init = init_params(1, rd2, np.zeros(2 * (n1 - n0), int), 1, P, K, seed=0)
+        shard = PertShard(1, rd2, data["gc"], np.zeros(2 * (n1 - n0), int), 1, P, K, init, cn_obs=st2,
+                          rep_obs=rep2, n_cells_total=2 * n_total, **common)
+    else:
+        kind = 2 if args.fit == "step2" else 3
+        init = init_params(kind, reads, libs, 1, P, K, ploidy=ploidy, t_init=t_init, beta_means=bm, seed=0)
+        extra = {}
+        if kind == 3:
+            from scdna_replication_tools_amd.simulator import convert_rt_units, load_bins
+            extra = dict(rho_fixed=convert_rt_units(load_bins(subdivide=subdiv)["mcf7rt"].to_numpy(np.float64)),
+                         a_fixed=10.0)
+        shard = PertShard(kind, reads, data["gc"], libs, 1, P, K, init, eta=eta, lamb=0.75, beta_means=bm,
+                          n_cells_total=n_total, **extra, **common)
     del data
     torch.cuda.synchronize()
 
@@ -196,13 +214,14 @@ def main():
     dt, kern_ms_max = float(t[0]), float(t[1])
 
     if rank == 0:
-        cellbins_total = L * n_total
+        cellbins_total = L * n_total * (2 if args.fit == "step1" else 1)
         value = cellbins_total * args.steps / dt
-        bpc = bytes_per_cellbin(P)
-        local_cb = L * (n1 - n0)
+        step1 = args.fit == "step1"
+        bpc = 4 + 1 + 1 if step1 else bytes_per_cellbin(P)      # step 1: reads + observed cn, rep (u8)
+        local_cb = L * (n1 - n0) * (2 if step1 else 1)
         achieved = bpc * local_cb / (kern_ms * 1e-3) / 1e9
         traffic = None
-        if os.path.exists(args.pmc):
+        if os.path.exists(args.pmc) and args.fit == "step2":
             try:
                 pm = json.load(open(args.pmc))
                 if pm.get("config") == args.config and int(pm.get("cells", -1)) == n1 - n0:
@@ -210,21 +229,23 @@ def main():
             except (OSError, ValueError):
                 traffic = None
         rec = {
-            "metric": "enumerated ELBO+grad cell*bins/s (10k cells x 5.5k bins, 500kb)",
+            "metric": ("enumerated ELBO+grad cell*bins/s (10k cells x 5.5k bins, 500kb)" if args.fit == "step2"
+                       else "{} SVI step cell*bins/s".format(args.fit)),
             "value": value, "unit": "cell*bins/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
             "scaling": args.scaling, "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": desc, "config": args.config, "cells": n_total, "bins": L, "P": P,
                        "K": K, "cn_prior": "g1_clones (weight 1e6)", "parallelism": "cell-sharded x{}".format(world),
-                       "bins_per_tile": shard.bins_per_tile},
+                       "bins_per_tile": shard.bins_per_tile, "fit": args.fit},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
-                         "kernel": ("enum_dma_kernel<13, STEP, 5>" if args.variant != 1 else "enum_kernel<13, STEP>"),
+                         "kernel": ("obs_kernel" if step1 else
+                                    "enum_dma_kernel<13, STEP, 5>" if args.variant != 1 else "enum_kernel<13, STEP>"),
                          "kernel_ms": kern_ms,
                          "bytes_per_cellbin": bpc},
             "loss_first": losses[0], "loss_last": losses[-1],
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.fit == "step2":
             data = synth(max(args.cpu_cells, 3), subdiv, seed=0, device=device)
             rec["cpu_baseline"] = cpu_baseline(data, args.cpu_cells, args.cpu_steps)
         else:

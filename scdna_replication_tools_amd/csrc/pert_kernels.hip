@@ -566,38 +566,78 @@ __global__ void __launch_bounds__(kBlock) obs_kernel(pert_problem pr, pert_state
   for (int k = 0; k < PERT_MAX_K1; ++k) acc[k] = 0.0f;
   float accT = 0.0f, loss = 0.0f, ga = 0.0f, dsum = 0.0f, gdd = 0.0f;
 
-  for (int l = l0; l < l1; ++l) {
+  // Per-bin constants of the tile (constrained rho, GC features) staged in LDS once: read per
+  // bin they would be scalar-cache loads whose latency every bin waits for.
+  __shared__ float s_bc[kMaxLT * (PERT_MAX_K1 + 1)];
+  for (int i = tid; i < (l1 - l0) * (K1 + 1); i += kBlock) {
+    const int lb = i / (K1 + 1), j = i - lb * (K1 + 1);
     float dm;
-    const float rho = clipped_sigmoid(st.params[lay.off_rho + l], &dm);
-    float g[PERT_MAX_K1];
+    s_bc[i] = j == 0 ? clipped_sigmoid(st.params[lay.off_rho + l0 + lb], &dm) : pr.gcf[(l0 + lb) * K1 + j - 1];
+  }
+  __syncthreads();
+
+  // Register software pipeline in groups of kObsU bins: the reads and observed states of the
+  // next group are loaded while the current group computes.  One bin of step-1 work (~150
+  // VALU) is far shorter than an HBM round trip under load, so the loads run kObsU bins
+  // ahead.  Rows are padded to ldn (every launched lane may load; only valid lanes add).
+  constexpr int kObsU = 4;
+  const float* __restrict__ reads = pr.reads;
+  const uint8_t* __restrict__ cno = pr.cn_obs;
+  const uint8_t* __restrict__ repo = pr.rep_obs;
+  float xq[kObsU];
+  uint32_t cq[kObsU], rq[kObsU];
+  auto load_group = [&](int lg) {
 #pragma unroll
-    for (int k = 0; k < PERT_MAX_K1; ++k) g[k] = (k < K1) ? pr.gcf[l * K1 + k] : 0.0f;
-    float gt = 0.0f;
-    if (valid) {
+    for (int u = 0; u < kObsU; ++u) {
+      const int l = min(lg + u, l1 - 1);
       const size_t ln = (size_t)l * pr.ldn + n;
-      const float x = pr.reads[ln];
-      const float invx = x > 0.0f ? 1.0f / x : 0.0f;
-      float dot = 0.0f;
-#pragma unroll
-      for (int k = 0; k < PERT_MAX_K1; ++k) dot += beta[k] * g[k];
-      const float omega = fexp(dot);
-      const float D = ucc * omega;
-      const float t = tau - rho;
-      const float phi = 1.0f / (1.0f + fexp(-a_val * t));
-      ObsOut o;
-      obs_cellbin(x, invx, (float)pr.cn_obs[ln], (float)pr.rep_obs[ln], log1m_lam, D, phi, o);
-      loss += o.ll;
-      gt = o.gt;
-      accT += a_val * o.gt;
-      ga += t * o.gt;
-      dsum += o.dsum;
-      gdd += o.gdd;
-      const float ge = o.gD * omega;
-#pragma unroll
-      for (int k = 0; k < PERT_MAX_K1; ++k) acc[k] += ge * g[k];
+      xq[u] = reads[ln];
+      cq[u] = cno[ln];
+      rq[u] = repo[ln];
     }
-    const float ws = wave_sum(gt);
-    if (lane == 0) s_bin[wave][l - l0] = ws;
+  };
+  if (l0 < l1) load_group(l0);
+
+  for (int lg = l0; lg < l1; lg += kObsU) {
+    float xg[kObsU], cg[kObsU], rg[kObsU];
+#pragma unroll
+    for (int u = 0; u < kObsU; ++u) { xg[u] = xq[u]; cg[u] = (float)cq[u]; rg[u] = (float)rq[u]; }
+    if (lg + kObsU < l1) load_group(lg + kObsU);
+#pragma unroll
+    for (int u = 0; u < kObsU; ++u) {
+      const int l = lg + u;
+      if (l >= l1) break;
+      const float x = xg[u], cnf = cg[u], repf = rg[u];
+      const float* bcl = s_bc + (l - l0) * (K1 + 1);
+      const float rho = bcl[0];
+      float g[PERT_MAX_K1];
+#pragma unroll
+      for (int k = 0; k < PERT_MAX_K1; ++k) g[k] = (k < K1) ? bcl[1 + k] : 0.0f;
+      float gt = 0.0f;
+      if (valid) {
+        const float invx = x > 0.0f ? frcp(x) : 0.0f;
+        float dot = 0.0f;
+#pragma unroll
+        for (int k = 0; k < PERT_MAX_K1; ++k) dot += beta[k] * g[k];
+        const float omega = fexp(dot);
+        const float D = ucc * omega;
+        const float t = tau - rho;
+        const float phi = 1.0f / (1.0f + fexp(-a_val * t));
+        ObsOut o;
+        obs_cellbin(x, invx, cnf, repf, log1m_lam, D, phi, o);
+        loss += o.ll;
+        gt = o.gt;
+        accT += a_val * o.gt;
+        ga += t * o.gt;
+        dsum += o.dsum;
+        gdd += o.gdd;
+        const float ge = o.gD * omega;
+#pragma unroll
+        for (int k = 0; k < PERT_MAX_K1; ++k) acc[k] += ge * g[k];
+      }
+      const float ws = wave_sum(gt);
+      if (lane == 0) s_bin[wave][l - l0] = ws;
+    }
   }
   __syncthreads();
   if (tid < l1 - l0) {

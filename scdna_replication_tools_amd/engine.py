@@ -129,6 +129,11 @@ def kappa_sum(reads: np.ndarray, log_lam: Optional[float]) -> float:
 
 
 # --------------------------------------------------------------------------- step-1 pi block
+# The canonical trajectory depends only on (P, lr, betas, eps): it is computed once per
+# process and shared by every step-1 fit (key -> per-step log pi~ and states).
+_PI_TRAJECTORIES: Dict[tuple, dict] = {}
+
+
 class CanonicalPiBlock:
     """Step 1's expose_pi site (pert_model.py:607-613 with etas = ones, cn observed).
 
@@ -136,7 +141,8 @@ class CanonicalPiBlock:
     density, starts at the uniform simplex for every (l, n), and Adam is
     element-wise, so every (l, n) follows the same trajectory up to a permutation
     of the states.  One P-vector reproduces all of them exactly; its loss term is
-    L * N * log pi~_c(t).
+    L * N * log pi~_c(t).  The trajectory is data independent, so it is computed once
+    (fp32 torch autograd + the Adam update below) and cached per (P, lr, betas, eps).
     """
 
     def __init__(self, P: int, lr: float, betas=ADAM_BETAS, eps=ADAM_EPS):
@@ -145,6 +151,7 @@ class CanonicalPiBlock:
         self.m = np.zeros(P, F32)
         self.v = np.zeros(P, F32)
         self.lr, self.b1, self.b2, self.eps = lr, betas[0], betas[1], eps
+        self.t = 0                               # Adam steps taken
 
     def logp_and_grad(self):
         z = torch.from_numpy(self.z.copy()).requires_grad_(True)
@@ -154,14 +161,7 @@ class CanonicalPiBlock:
         lp.backward()
         return float(lp.detach()), (-z.grad).numpy().astype(F32)             # loss gradient
 
-    def trajectory(self, t0: int, n: int) -> np.ndarray:
-        """log pi~ of steps t0 .. t0+n-1 (the values ``step`` would return), without
-        advancing this block: the per-step loss term of a device-side SVI loop."""
-        blk = CanonicalPiBlock(self.P, self.lr, (self.b1, self.b2), self.eps)
-        blk.z, blk.m, blk.v = self.z.copy(), self.m.copy(), self.v.copy()
-        return np.array([blk.step(t0 + i) for i in range(n)], dtype=np.float64)
-
-    def step(self, t: int) -> float:
+    def _advance(self, t: int) -> float:
         lp, g = self.logp_and_grad()
         self.m = (self.b1 * self.m + (1 - self.b1) * g).astype(F32)
         self.v = (self.b2 * self.v + (1 - self.b2) * g * g).astype(F32)
@@ -170,6 +170,47 @@ class CanonicalPiBlock:
         denom = np.sqrt(self.v) / math.sqrt(bc2) + self.eps
         self.z = (self.z - (self.lr / bc1) * self.m / denom).astype(F32)
         return lp
+
+    def _cache(self, T: int) -> dict:
+        """The shared trajectory, extended to at least T steps."""
+        key = (self.P, float(self.lr), float(self.b1), float(self.b2), float(self.eps))
+        c = _PI_TRAJECTORIES.get(key)
+        if c is None:
+            c = _PI_TRAJECTORIES[key] = {"lp": [], "state": [(self.__class__(self.P, self.lr, (self.b1, self.b2),
+                                                                                self.eps).z, np.zeros(self.P, F32),
+                                                               np.zeros(self.P, F32))]}
+        if len(c["lp"]) < T:
+            w = CanonicalPiBlock.__new__(CanonicalPiBlock)
+            w.P, w.lr, w.b1, w.b2, w.eps = self.P, self.lr, self.b1, self.b2, self.eps
+            w.z, w.m, w.v = (a.copy() for a in c["state"][-1])
+            while len(c["lp"]) < T:
+                c["lp"].append(w._advance(len(c["lp"]) + 1))
+                c["state"].append((w.z.copy(), w.m.copy(), w.v.copy()))
+        return c
+
+    def trajectory(self, t0: int, n: int) -> np.ndarray:
+        """log pi~ of steps t0 .. t0+n-1 (the values ``step`` would return), without
+        advancing this block: the per-step loss term of a device-side SVI loop."""
+        if t0 != self.t + 1:
+            raise ValueError("the block is at step {}, not {}".format(self.t, t0 - 1))
+        c = self._cache(t0 - 1 + n)
+        return np.asarray(c["lp"][t0 - 1:t0 - 1 + n], dtype=np.float64)
+
+    def step(self, t: int) -> float:
+        """Adam step t (= previous step + 1); returns log pi~ before the update."""
+        if t != self.t + 1:
+            raise ValueError("the block is at step {}, not {}".format(self.t, t - 1))
+        c = self._cache(t)
+        self.z, self.m, self.v = (a.copy() for a in c["state"][t])
+        self.t = t
+        return c["lp"][t - 1]
+
+    def advance_to(self, t: int) -> float:
+        """Take steps up to t at once; returns the last step's log pi~."""
+        c = self._cache(t)
+        self.z, self.m, self.v = (a.copy() for a in c["state"][t])
+        self.t = t
+        return c["lp"][t - 1] if t > 0 else float("nan")
 
 
 # --------------------------------------------------------------------------- shard
@@ -510,9 +551,8 @@ class PertShard:
         n_done = stop_at + 1 if stop_at >= 0 else launched
         losses = host[:n_done, 0].tolist()
         self.t = t0 + n_done
-        if self.pi_block is not None:
-            for k in range(n_done):
-                self._pi_lp = self.pi_block.step(t0 + 1 + k)
+        if self.pi_block is not None and n_done > 0:
+            self._pi_lp = self.pi_block.advance_to(t0 + n_done)
         return losses, (reason if stop_at >= 0 else 0)
 
     def device_loss(self) -> float:

@@ -8,7 +8,7 @@ OUT=$R/gpurun_out/pmcq_$TAG
 mkdir -p "$OUT"
 ARGS=${*:-"--steps 5 --warmup 1 --no-cpu-baseline"}
 cd /tmp && export TMPDIR=/tmp
-K='--kernel-include-regex enum_dma'
+K="--kernel-include-regex ${KREGEX:-enum_dma}"
 i=0
 for PMC in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_LDS" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do

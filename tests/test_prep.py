@@ -148,3 +148,20 @@ def test_package_output_keys_path_matches_lookup_path():
     n = list(inp.cells_s).index(r["cell_id"])
     l = [i for i in range(L) if inp.loci_chr[i] == str(r["chr"]) and inp.loci_start[i] == r["start"]][0]
     assert r["model_cn_state"] == cn[l, n] and r["model_rep_state"] == rep[l, n]
+
+
+def test_consensus_matches_reference_golden():
+    """prep.consensus_clone_profiles against the reference's own compute_consensus_clone_profiles
+    output (tests/golden/make_reference_golden.py; cn_state_col=None path, unsorted rows,
+    missing rows, a 'None' clone)."""
+    import os
+    import pandas as pd
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "consensus_reference.npz"))
+    df = pd.DataFrame({"cell_id": g["cell_id"].astype(object), "chr": g["chr"].astype(object), "start": g["start"],
+                       "clone_id": g["clone_id"].astype(object), "copy": g["copy"]})
+    got = prep.consensus_clone_profiles(df, "copy", clone_col="clone_id", cell_col="cell_id", chr_col="chr",
+                                        start_col="start", cn_state_col=None)
+    assert list(np.asarray(got.columns).astype(str)) == list(g["prof_clones"])
+    assert list(np.asarray(got.index.get_level_values(0)).astype(str)) == list(g["prof_chr"])
+    assert (np.asarray(got.index.get_level_values(1)) == g["prof_start"]).all()
+    np.testing.assert_array_equal(got.to_numpy(np.float64), g["prof_values"])

@@ -61,7 +61,11 @@ PERT_HD float log1p_corr(float q, float inv_u) {
   return flog(u) + (q - (u - 1.0f)) * inv_u;
 }
 
-// Stirling remainder S(z) = 1/(12 z) - 1/(360 z^3) + 1/(1260 z^5), z >= 8 (|err| < 4e-10).
+// Stirling remainder S(z) = 1/(12 z) - 1/(360 z^3) + 1/(1260 z^5): truncation error below
+// 1/(1680 z^7), 7.6e-9 at z = 5 (kAsymMin); the digamma series below (to 1/(252 z^6)) below
+// 1/(240 z^8), 1.1e-8 at z = 5.
+constexpr float kAsymMin = 5.0f;   // asymptotic series used for arguments >= kAsymMin
+constexpr float kShift = 4.0f;     // 1 <= d < kAsymMin is shifted by kShift (d + kShift >= kAsymMin)
 PERT_HD float stirling_rem(float rz) {
   float rz2 = rz * rz;
   return rz * (0.0833333333333333333f - rz2 * (0.00277777777777777778f - rz2 * 0.000793650793650793651f));
@@ -70,12 +74,12 @@ PERT_HD float stirling_rem(float rz) {
 // Lambda(d, x) = lgamma(d+x) - lgamma(d) - (x log x - x)  and  Psi(d, x) = digamma(d+x) - digamma(d)
 // for d >= 1, x >= 0 (x integer valued as in pert_model.py:163-166; any x >= 0 works).
 // invx = 1/x (0 when x == 0).
-//   d >= 8: asymptotic series on both arguments in cancellation-free form
+//   d >= kAsymMin: asymptotic series on both arguments in cancellation-free form
 //     (d - 1/2) log1p(x/d) + x log1p(d/x) + S(d+x) - S(d)
-//   d <  8: shift d by 7 with the recurrences (nb_shift7)
-//     lgamma(y) = lgamma(y + 7) - log prod_{i<7} (y + i),  digamma(y) = digamma(y + 7) - sum 1/(y + i).
+//   d <  kAsymMin: shift d by kShift with the recurrences (nb_shift)
+//     lgamma(y) = lgamma(y + 4) - log prod_{i<4} (y + i),  digamma(y) = digamma(y + 4) - sum 1/(y + i).
 PERT_HD void nb_lgdiff_asym(float d, float x, float invx, float& lam, float& psi) {
-  // d >= 8 (no branches)
+  // d >= kAsymMin (no branches)
   const float r = frcp(d);
   const float zs = d + x;
   const float rz = frcp(zs);
@@ -88,7 +92,7 @@ PERT_HD void nb_lgdiff_asym(float d, float x, float invx, float& lam, float& psi
         + 0.00833333333333333333f * (rz4 - r4) - 0.00396825396825396825f * (rz4 * rz2 - r4 * r2);
 }
 
-// nb_lgdiff_asym for d = chi D >= 8 with the per-(bin, cell) invariants hoisted out of
+// nb_lgdiff_asym for d = chi D >= kAsymMin with the per-(bin, cell) invariants hoisted out of
 // the chi loop: r = 1/d = (1/D)(1/chi) (one v_rcp per cell.bin instead of per chi) and
 // log1p(d/x) = log1p(x/d) + log(d/x), log(d/x) = log(chi) + (log D - log x) (no second
 // v_log per chi).  ldxc = log(d/x) (any finite value when x == 0: it is multiplied by x).
@@ -104,33 +108,27 @@ PERT_HD void nb_lgdiff_asym_hoisted(float d, float r, float x, float ldxc, float
         + 0.00833333333333333333f * (rz4 - r4) - 0.00396825396825396825f * (rz4 * rz2 - r4 * r2);
 }
 
-// 1 <= d < 8: shift by exactly 7 (d + 7 >= 8 for every d >= 1, so no per-lane shift count)
-// with the products A = prod_{i<7} (d+i), B = prod_{i<7} (d+x+i) and their d-derivatives
-// carried along (one fma + one mul per factor, no per-factor reciprocal):
-//   lgamma(d+x) - lgamma(d) = [lgamma(d+7+x) - lgamma(d+7)] - log(B / A)
-//   psi(d+x) - psi(d)       = [psi(d+7+x) - psi(d+7)] - B'/B + A'/A
-// The factors go in two groups (i < 4, i >= 4), each ratio B_g / A_g <= (1 + x)^4, so
-// nothing overflows for any count x < 4e9, and x = 0 gives exactly zero corrections.
-PERT_HD void nb_shift7(float d, float x, float& corr_l, float& corr_p) {
-  float A[2] = {1.0f, 1.0f}, Ap[2] = {0.0f, 0.0f}, B[2] = {1.0f, 1.0f}, Bp[2] = {0.0f, 0.0f};
+// 1 <= d < kAsymMin: shift by exactly kShift = 4 (d + 4 >= 5 for every d >= 1, so no per-lane
+// shift count) with the products A = prod_{i<4} (d+i), B = prod_{i<4} (d+x+i) and their
+// d-derivatives carried along (one fma + one mul per factor, no per-factor reciprocal):
+//   lgamma(d+x) - lgamma(d) = [lgamma(d+4+x) - lgamma(d+4)] - log(B / A)
+//   psi(d+x) - psi(d)       = [psi(d+4+x) - psi(d+4)] - B'/B + A'/A
+// B / A <= (1 + x)^4, so nothing overflows for any count x < 4e9, and x = 0 gives exactly zero
+// corrections (2 v_rcp + 1 v_log per shifted argument).
+PERT_HD void nb_shift(float d, float x, float& corr_l, float& corr_p) {
+  float A = 1.0f, Ap = 0.0f, B = 1.0f, Bp = 0.0f;
 #pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    const int g = i < 4 ? 0 : 1;
+  for (int i = 0; i < 4; ++i) {
     const float a = d + (float)i;
     const float b = a + x;
-    Ap[g] = Ap[g] * a + A[g];
-    A[g] *= a;
-    Bp[g] = Bp[g] * b + B[g];
-    B[g] *= b;
+    Ap = Ap * a + A;
+    A *= a;
+    Bp = Bp * b + B;
+    B *= b;
   }
-  corr_l = 0.0f;
-  corr_p = 0.0f;
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    const float rA = frcp(A[g]);
-    corr_l -= flog(B[g] * rA);
-    corr_p += Ap[g] * rA - Bp[g] * frcp(B[g]);
-  }
+  const float rA = frcp(A);
+  corr_l = -flog(B * rA);
+  corr_p = Ap * rA - Bp * frcp(B);
   // x = 0: B = A, so both corrections are exactly 0 (fma contraction would leave ~1 ulp)
   corr_l = x > 0.0f ? corr_l : 0.0f;
   corr_p = x > 0.0f ? corr_p : 0.0f;
@@ -138,9 +136,9 @@ PERT_HD void nb_shift7(float d, float x, float& corr_l, float& corr_p) {
 
 PERT_HD void nb_lgdiff(float d, float x, float invx, float& lam, float& psi) {
   float corr_l = 0.0f, corr_p = 0.0f;
-  if (d < 8.0f) {
-    nb_shift7(d, x, corr_l, corr_p);
-    d += 7.0f;
+  if (d < kAsymMin) {
+    nb_shift(d, x, corr_l, corr_p);
+    d += kShift;
   }
   nb_lgdiff_asym(d, x, invx, lam, psi);
   lam += corr_l;
@@ -252,8 +250,8 @@ PERT_HD void enum_forward(float x, float invx, const float (&z)[P], float log1m_
   s[0] += n_clamped;
   s[P] += n_clamped;
   Bc[0] = 0.0f;
-  if (D >= 8.0f) {
-    // every delta = chi D >= 8: straight-line asymptotic series, no clamp, no shift --
+  if (D >= kAsymMin) {
+    // every delta = chi D >= kAsymMin: straight-line asymptotic series, no clamp, no shift --
     // one basic block, so the 2P-2 independent chains interleave (ILP)
     const float rD = frcp(D);
     const float ldx = x > 0.0f ? flog(D) - flog(x) : 0.0f;

@@ -274,6 +274,24 @@ __global__ void __launch_bounds__(kBlock, 2) enum_kernel(pert_problem pr, pert_s
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
+// Cache policy of the streamed traffic: every byte of the pi state, reads and eta codes is
+// touched once per pass, so the HBM -> LDS copies are non-temporal (aux = 2, `nt`) and so are
+// the pi-state stores.  Both together: -1.8 % kernel at C4, -1.6 % at 1,250 cells (A/B on one
+// box, two interleaved rounds); either alone is within noise.
+#ifndef PERT_DMA_AUX
+#define PERT_DMA_AUX 2
+#endif
+#ifndef PERT_NT_STORE
+#define PERT_NT_STORE 1
+#endif
+__device__ __forceinline__ void store_stream(float* p, float v) {
+#if PERT_NT_STORE
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 template <int BYTES>
 __device__ __forceinline__ void dma_run(const void* gsrc, float* ldst, int lane) {
   // a contiguous run of BYTES (multiple of 128) -> the same bytes at ldst
@@ -282,17 +300,17 @@ __device__ __forceinline__ void dma_run(const void* gsrc, float* ldst, int lane)
   constexpr int rem = BYTES % 1024;
 #pragma unroll
   for (int i = 0; i < n16; ++i)
-    __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g + i * 1024 + lane * 16), (lds_ptr_t)(ldst + i * 256), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g + i * 1024 + lane * 16), (lds_ptr_t)(ldst + i * 256), 16, 0, PERT_DMA_AUX);
   if constexpr (rem >= 256) {
 #pragma unroll
     for (int i = 0; i < rem / 256; ++i)
       __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g + n16 * 1024 + i * 256 + lane * 4),
-                                       (lds_ptr_t)(ldst + n16 * 256 + i * 64), 4, 0, 0);
+                                       (lds_ptr_t)(ldst + n16 * 256 + i * 64), 4, 0, PERT_DMA_AUX);
   }
   if constexpr (rem % 256 == 128) {
     // 128-B tail: 4-B pieces on half the wave (sub-dword LDS-DMA is not lane-packed)
     if (lane < 32)
-      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g + BYTES - 128 + lane * 4), (lds_ptr_t)(ldst + (BYTES - 128) / 4), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g + BYTES - 128 + lane * 4), (lds_ptr_t)(ldst + (BYTES - 128) / 4), 4, 0, PERT_DMA_AUX);
   }
 }
 
@@ -478,9 +496,9 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
           const float m1 = hp.beta1 * mb[k * 64 + lane] + (1.0f - hp.beta1) * gl;
           const float v1 = hp.beta2 * mb[ZF + k * 64 + lane] + (1.0f - hp.beta2) * gl * gl;
           const float denom = __builtin_sqrtf(v1) * hp.inv_bc2_sqrt + hp.eps;
-          zo[k * 64] = zt[k] - hp.step_size * m1 * frcp(denom);
-          mo[k * 64] = m1;
-          vo[k * 64] = v1;
+          store_stream(zo + k * 64, zt[k] - hp.step_size * m1 * frcp(denom));
+          store_stream(mo + k * 64, m1);
+          store_stream(vo + k * 64, v1);
         }
       } else {
         float* gp = st.g_pi + tile + lane;

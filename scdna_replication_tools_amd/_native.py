@@ -76,19 +76,25 @@ _lib = None
 def lib():
     """Load libpert_hip.so once; raise loudly if it is absent or incomplete."""
     global _lib
-    if _lib is not None:
-        return _lib
+    if _lib is None:
+        _lib = load(LIB_PATH)
+    return _lib
+
+
+def load(path: str):
+    """Load and type one build of the C ABI (``lib()`` is the product one; A/B tools load
+    a second build beside it)."""
     # torch first: its bundled libamdhip64 (soname libamdhip64.so.7) must be the one HIP
     # runtime of the process, so our kernels and torch's allocations share a context.
     import torch  # noqa: F401
-    if not os.path.exists(LIB_PATH):
+    if not os.path.exists(path):
         raise NativeLibraryError(
             "{} not found: the PERT HIP extension is not built (run "
-            "`python -m scdna_replication_tools_amd.build`). There is no CPU fallback.".format(LIB_PATH))
+            "`python -m scdna_replication_tools_amd.build`). There is no CPU fallback.".format(path))
     try:
-        handle = ctypes.CDLL(LIB_PATH)
+        handle = ctypes.CDLL(path)
     except OSError as e:  # pragma: no cover
-        raise NativeLibraryError("failed to load {}: {}".format(LIB_PATH, e))
+        raise NativeLibraryError("failed to load {}: {}".format(path, e))
     missing = [s for s in EXPORTED_SYMBOLS if not hasattr(handle, s)]
     if missing:
         raise NativeLibraryError("{} lacks symbols {}".format(LIB_PATH, missing))
@@ -111,8 +117,7 @@ def lib():
     for name in EXPORTED_SYMBOLS:
         if name != "pert_version":
             getattr(handle, name).restype = c_int32
-    _lib = handle
-    return _lib
+    return handle
 
 
 def check(code: int, what: str):
@@ -135,10 +140,11 @@ def workspace_sizes(kind: int, L: int, N: int, K1: int, n_libs: int, bins_per_ti
     return tuple(int(o.value) for o in out)
 
 
-def auto_bins_per_tile(prob: PertProblem, variant: int = 0) -> int:
+def auto_bins_per_tile(prob: PertProblem, variant: int = 0, handle=None) -> int:
     """pert_auto_bins_per_tile: occupancy-aware tile length on the current device."""
     out = c_int32()
-    check(lib().pert_auto_bins_per_tile(ctypes.byref(prob), int(variant), ctypes.byref(out)),
+    h = lib() if handle is None else handle
+    check(h.pert_auto_bins_per_tile(ctypes.byref(prob), int(variant), ctypes.byref(out)),
           "pert_auto_bins_per_tile")
     return int(out.value)
 

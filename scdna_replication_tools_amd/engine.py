@@ -227,8 +227,8 @@ class PertShard:
                  pi_init=None, device=None, lr: float = 0.05, betas=ADAM_BETAS, eps: float = ADAM_EPS,
                  is_root: bool = True, n_cells_total: Optional[int] = None,
                  allreduce: Optional[Callable[[torch.Tensor], None]] = None,
-                 dirichlet_mode: str = "torch32", bins_per_tile: int = 0, variant: int = 0):
-        self.lib = nat.lib()
+                 dirichlet_mode: str = "torch32", bins_per_tile: int = 0, variant: int = 0, lib=None):
+        self.lib = nat.lib() if lib is None else lib        # another build of the ABI (A/B tools)
         self.kind = int(kind)
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
@@ -342,7 +342,7 @@ class PertShard:
             beta_means=_ptr(self.beta_means_t), rho_fixed=_ptr(self.rho_fixed_t))
         if bins_per_tile <= 0:
             with self._dev():
-                bins_per_tile = nat.auto_bins_per_tile(self._prob, variant)
+                bins_per_tile = nat.auto_bins_per_tile(self._prob, variant, self.lib)
         ncp, nbp, nblk, ncb = nat.workspace_sizes(self.kind, L, N, self.K1, self.n_libs, bins_per_tile)
         self.cell_part = torch.zeros(ncp, **f32)
         self.bin_part = torch.zeros(nbp, **f32)

@@ -220,14 +220,15 @@ def main():
         bpc = 4 + 1 + 1 if step1 else bytes_per_cellbin(P)      # step 1: reads + observed cn, rep (u8)
         local_cb = L * (n1 - n0) * (2 if step1 else 1)
         achieved = bpc * local_cb / (kern_ms * 1e-3) / 1e9
-        traffic = None
+        traffic, valu = None, None
         if os.path.exists(args.pmc) and args.fit == "step2":
             try:
                 pm = json.load(open(args.pmc))
                 if pm.get("config") == args.config and int(pm.get("cells", -1)) == n1 - n0:
                     traffic = pm.get("hbm_bytes_per_launch")
+                    valu = pm.get("valu")
             except (OSError, ValueError):
-                traffic = None
+                traffic, valu = None, None
         rec = {
             "metric": ("enumerated ELBO+grad cell*bins/s (10k cells x 5.5k bins, 500kb)" if args.fit == "step2"
                        else "{} SVI step cell*bins/s".format(args.fit)),
@@ -242,7 +243,10 @@ def main():
                          "kernel": ("obs_kernel" if step1 else
                                     "enum_dma_kernel<13, STEP, 5>" if args.variant != 1 else "enum_kernel<13, STEP>"),
                          "kernel_ms": kern_ms,
-                         "bytes_per_cellbin": bpc},
+                         "bytes_per_cellbin": bpc,
+                         # PMC (profiles/pmc_traffic.json, tools/profile.sh): VALU issue fraction of
+                         # the same kernel -- the other roofline, not the binding one here
+                         "valu_issue_frac": (valu or {}).get("issue_frac")},
             "loss_first": losses[0], "loss_last": losses[-1],
         }
         if world == 1 and not args.no_cpu_baseline and args.fit == "step2":

@@ -1,0 +1,75 @@
+"""GPU edge cases of the C-ABI path against the fp64 oracle: the smallest shapes (one cell,
+two bins -- one bin makes the simulator's min-max RT scaling 0/0), cell counts off the 64-lane tile and bin counts off the tile length, P = 2 and
+P = 16, K = 1 and K = 7 (the generic K1 instance), all-zero and very large read counts,
+and the refused empty shard."""
+import numpy as np
+import pytest
+
+from oracle import pert_oracle as po
+from tests._problems import KIND_OF, init_constrained, make_problem
+
+pytestmark = pytest.mark.gpu
+
+
+def _shard(kind, kw, z, **extra):
+    from scdna_replication_tools_amd.engine import PertShard
+    sh = PertShard(KIND_OF[kind], init=init_constrained(kind, z), device="cuda", dirichlet_mode="exact",
+                   **kw, **extra)
+    sh.set_unconstrained({k: v.numpy() for k, v in z.items()})
+    return sh
+
+
+def _check(kind, prob, kw, z, loss_rtol=1e-5, grad_rtol=1e-4, **extra):
+    ref_loss, ref_g = po.loss_and_grads(prob, z)
+    sh = _shard(kind, kw, z, **extra)
+    loss, g = sh.loss_and_grads()
+    assert np.isfinite(loss)
+    assert abs(loss - float(ref_loss)) <= loss_rtol * abs(float(ref_loss)), (loss, float(ref_loss))
+    for name, gref in ref_g.items():
+        if kind == "step1" and name == "expose_pi":
+            continue
+        a, b = np.asarray(g[name], np.float64), gref.numpy()
+        r = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+        assert r <= grad_rtol, (name, r)
+    if kind != "step1":
+        cn_ref, rep_ref = po.decode(prob, z)
+        cn, rep = _shard(kind, kw, z, **extra).decode()
+        agree = (cn.cpu().numpy() == cn_ref.numpy()) & (rep.cpu().numpy() == rep_ref.numpy())
+        assert agree.mean() >= 0.99, agree.mean()
+
+
+@pytest.mark.parametrize("kind", ["step2", "step1"])
+@pytest.mark.parametrize("L,N,P,K", [(2, 1, 13, 4), (3, 65, 13, 4), (70, 257, 2, 1), (5, 64, 16, 7)])
+def test_shapes(kind, L, N, P, K):
+    prob, kw, z = make_problem(kind, L=L, N=N, P=P, K=K, n_libs=1, seed=L + N)
+    _check(kind, prob, kw, z)
+
+
+def test_bins_off_the_tile_length():
+    prob, kw, z = make_problem("step2", L=65, N=130, n_libs=1, seed=9)
+    _check("step2", prob, kw, z, bins_per_tile=64)          # one 64-bin tile and a 1-bin tile
+
+
+@pytest.mark.parametrize("kind", ["step2", "step1"])
+def test_mostly_zero_reads(kind):
+    """High-zero-count regime (x = 0 in 9 of 10 bins; a cell with no reads at all is degenerate
+    in the reference itself: u ~ Normal(0, 0))."""
+    keep = lambda r: np.where(np.arange(r.shape[0])[:, None] % 10 == 0, r, 0.0)
+    prob, kw, z = make_problem(kind, L=30, N=40, n_libs=1, seed=3, reads_fn=keep)
+    _check(kind, prob, kw, z)
+
+
+def test_very_large_counts():
+    """~9e3 reads per bin (50x the 500 kb coverage of a 1e6-read cell)."""
+    prob, kw, z = make_problem("step2", L=12, N=40, n_libs=1, seed=4, reads_fn=lambda r: r * 50 + 1)
+    _check("step2", prob, kw, z, loss_rtol=2e-5)
+
+
+def test_empty_shard_is_refused():
+    from scdna_replication_tools_amd.engine import PertShard
+    prob, kw, z = make_problem("step2", L=4, N=6, n_libs=1, seed=1)
+    kw = dict(kw)
+    kw["reads"] = np.zeros((4, 0))
+    kw["libs"] = np.zeros(0, int)
+    with pytest.raises(ValueError):
+        PertShard(2, init=init_constrained("step2", z), device="cuda", **kw)

@@ -34,16 +34,36 @@ def _chr_codes(chrc: pd.Series) -> np.ndarray:
         cats = np.asarray(chrc.cat.categories)
         codes = chrc.cat.codes.to_numpy().astype(np.int64)
     else:
-        codes, cats = pd.factorize(chrc.to_numpy())
+        codes, cats = _factorize(chrc.to_numpy())
         codes = codes.astype(np.int64)
     pos = {c: i for i, c in enumerate(CHR_ORDER)}
     lut = np.array([pos.get(str(c), -1) for c in cats] + [-1], dtype=np.int64)
     return lut[np.where(codes >= 0, codes, len(cats))]
 
 
+def _factorize(values, sort: bool = False):
+    """pd.factorize, but for object (string) columns that come in runs -- a long-form table
+    grouped by cell, or by chromosome -- only the run heads are hashed: an adjacent-element
+    comparison costs a fraction of hashing every Python string."""
+    v = np.asarray(values)
+    if v.dtype != object or v.size < (1 << 16):
+        return pd.factorize(v, sort=sort)
+    probe = v[:1 << 16]
+    if np.count_nonzero(probe[1:] != probe[:-1]) > probe.size // 8:
+        return pd.factorize(v, sort=sort)
+    change = np.empty(v.size, dtype=bool)
+    change[0] = True
+    np.not_equal(v[1:], v[:-1], out=change[1:])
+    heads = np.flatnonzero(change)
+    if heads.size > v.size // 8:
+        return pd.factorize(v, sort=sort)
+    codes, uniq = pd.factorize(v[heads], sort=sort)
+    return np.repeat(codes, np.diff(np.append(heads, v.size))), uniq
+
+
 def _sorted_codes(values) -> tuple:
     """(codes, sorted uniques) with NaN keys coded -1, like pandas' sorted group keys."""
-    codes, uniq = pd.factorize(np.asarray(values), sort=True)
+    codes, uniq = _factorize(values, sort=True)
     return codes.astype(np.int64), np.asarray(uniq)
 
 
@@ -66,7 +86,7 @@ def _sorted_table(cn: pd.DataFrame, cell_col: str, chr_col: str, start_col: str,
     if notna_col is not None:
         order = order[cn[notna_col].notna().to_numpy()[order]]
     if order.size == len(cn) and (order.size == 0 or (order[1:] > order[:-1]).all()):
-        out = cn.copy()                                  # already sorted and complete: no gather
+        out = cn.copy(deep=False)                        # already sorted and complete: no gather
     else:
         out = cn.take(order)
     out[chr_col] = pd.Categorical.from_codes(ch[order], categories=CHR_ORDER)
@@ -190,7 +210,7 @@ def _align(p: Pivot, chr_, start) -> Pivot:
 def _cell_libraries(cn: pd.DataFrame, keys: TableKeys, library_col: str, cells: np.ndarray):
     """(cell, library) pairs of get_libraries_tensor (:206-225) from the integer keys:
     the library labels in first-appearance order and one label per pivot cell."""
-    lib_code, lib_uniq = pd.factorize(cn[library_col].to_numpy())
+    lib_code, lib_uniq = _factorize(cn[library_col].to_numpy())
     cc = keys.cell_code
     ok = cc >= 0
     pairs = pd.unique(cc[ok] * (len(lib_uniq) + 1) + lib_code[ok])
@@ -274,7 +294,7 @@ def _majority_ploidy_rows(cn: pd.DataFrame, clone_col="clone_id", cell_col="cell
         cell_code, cells = _sorted_codes(cn[cell_col].to_numpy())
         n_cells = len(cells)
     if clone_code is None:
-        clone_code, ku = pd.factorize(cn[clone_col].to_numpy())
+        clone_code, ku = _factorize(cn[clone_col].to_numpy())
         n_clones = len(ku)
     cc, kc = cell_code, clone_code
     pl_cell = _cell_mode(cc, n_cells, cn[cn_state_col].to_numpy())
@@ -292,7 +312,7 @@ def filter_ploidies(cn: pd.DataFrame, ploidy: Optional[pd.Series] = None, clone_
     if ploidy is None:
         return cn[_majority_ploidy_rows(cn, clone_col, cell_col, cn_state_col)]
     pl = cn[cell_col].map(ploidy).to_numpy()
-    kc, ku = pd.factorize(cn[clone_col].to_numpy())
+    kc, ku = _factorize(cn[clone_col].to_numpy())
     pc, pu = pd.factorize(pl, sort=True)
     ok = (kc >= 0) & (pc >= 0)
     cnt = np.bincount(kc[ok] * len(pu) + pc[ok], minlength=len(ku) * len(pu)).reshape(len(ku), len(pu))
@@ -333,7 +353,7 @@ def consensus_clone_profiles(cn: pd.DataFrame, col_name: str, clone_col="clone_i
             cc, cells = _sorted_codes(cn[cell_col].to_numpy())
         cc = np.where(rows, cc, -1)
         rows &= _majority_ploidy_rows(cn, clone_col, cell_col, cn_state_col, cc, len(cells), kc, len(ku))
-    hc, hu = pd.factorize(cn[chr_col])
+    hc, hu = _factorize(cn[chr_col].to_numpy())
     st = cn[start_col].to_numpy()
     ok = hc >= 0
     lc, lu = pd.factorize(np.where(ok, hc.astype(np.int64) * (1 << 40) + np.where(ok, st, 0).astype(np.int64), -1))

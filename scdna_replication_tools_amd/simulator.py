@@ -143,14 +143,19 @@ def simulate(n_s: int, n_g: Optional[int] = None, n_bins: Optional[int] = None, 
                          clone_g=clone_g, clone_cn=prof)
 
 
-def to_long_form(sim: SyntheticPERT, input_col: str = "reads", n_libs: int = 1, copy_from: str = "state"):
+def to_long_form(sim: SyntheticPERT, input_col: str = "reads", n_libs: int = 1, copy_from: str = "state",
+                 order: str = "cell"):
     """Long-form DataFrames (one row per cell x bin) with the columns the
     reference entry points consume (``pert_infer_scRT``, pert_model.py:37-43) plus
     the simulator's truth columns (pert_simulator.py:371-418).
 
     ``copy`` (HMMcopy's copy-number estimate, the default ``assign_col``) is the true
     state (``copy_from='state'``) or a noisy estimate from the reads: each cell's reads
-    scaled to its mean state (``copy_from='reads'``, what clustering needs)."""
+    scaled to its mean state (``copy_from='reads'``, what clustering needs).
+
+    ``order='cell'``: rows grouped by cell, bins in genome order within a cell (per-cell
+    HMMcopy tables concatenated, as the reference simulator's per-clone merges produce);
+    ``order='bin'``: rows grouped by bin."""
     import pandas as pd
     L = sim.n_bins
     clone_names = np.array([chr(ord("A") + i) for i in range(sim.clone_cn.shape[1])])
@@ -165,22 +170,33 @@ def to_long_form(sim: SyntheticPERT, input_col: str = "reads", n_libs: int = 1, 
         else:
             raise ValueError(copy_from)
         cells = np.array(["cell_{}_{}".format(prefix, i) for i in range(n)])
+        libs = np.array(["LIB{}".format(i % n_libs) for i in range(n)])
+        if order == "cell":
+            per_bin = lambda a: np.tile(a, n)                 # (L,) bin attribute -> rows
+            per_cell = lambda a: np.repeat(a, L)              # (n,) cell attribute -> rows
+            flat = lambda a: np.asarray(a).T.reshape(-1)      # (L, n) matrix -> rows
+        elif order == "bin":
+            per_bin = lambda a: np.repeat(a, n)
+            per_cell = lambda a: np.tile(a, L)
+            flat = lambda a: np.asarray(a).reshape(-1)
+        else:
+            raise ValueError(order)
         d = {
-            "cell_id": np.tile(cells, L),
-            "chr": np.repeat(sim.chrom, n),
-            "start": np.repeat(sim.start, n),
-            "gc": np.repeat(sim.gc, n),
-            "mcf7rt": np.repeat(sim.rt, n),
-            "library_id": np.tile(np.array(["LIB{}".format(i % n_libs) for i in range(n)]), L),
-            "clone_id": np.tile(clone_names[clone], L),
-            "state": cn.reshape(-1).astype(np.int64),
-            "copy": copy.reshape(-1),
-            input_col: reads.reshape(-1),
-            "true_somatic_cn": cn.reshape(-1),
+            "cell_id": per_cell(cells),
+            "chr": per_bin(sim.chrom),
+            "start": per_bin(sim.start),
+            "gc": per_bin(sim.gc),
+            "mcf7rt": per_bin(sim.rt),
+            "library_id": per_cell(libs),
+            "clone_id": per_cell(clone_names[clone]),
+            "state": flat(cn).astype(np.int64),
+            "copy": flat(copy),
+            input_col: flat(reads),
+            "true_somatic_cn": flat(cn),
         }
         if rep is not None:
-            d["true_rep"] = rep.reshape(-1)
-            d["true_t"] = np.tile(tau, L)
+            d["true_rep"] = flat(rep)
+            d["true_t"] = per_cell(tau)
         else:
             d["true_rep"] = np.zeros(L * n)
             d["true_t"] = np.zeros(L * n)

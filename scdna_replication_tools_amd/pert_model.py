@@ -253,7 +253,10 @@ class pert_infer_scRT():
             'model_rho': np.asarray(fit["expose_rho"], dtype=np.float32).reshape(-1)[li],
         })
         # new columns side by side with the (sorted) input rows, without copying its blocks
-        out = pd.concat([base.reset_index(drop=True), model], axis=1, copy=False)
+        # (reset_index(drop=True) would deep-copy and consolidate the whole long table)
+        base = base.copy(deep=False)
+        base.index = pd.RangeIndex(len(base))
+        out = pd.concat([base, model], axis=1, copy=False)
         supp = pd.concat([
             pd.DataFrame({'param': ['model_lambda'], 'level': ['all'], 'value': [float(lambda_fit[0])]}),
             pd.DataFrame({'param': ['model_a'], 'level': ['all'], 'value': [float(np.asarray(fit["expose_a"])[0])]}),

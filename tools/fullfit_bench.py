@@ -45,6 +45,9 @@ def main():
     t_sim = time.perf_counter() - t0
     print("simulated {} + {} cells x {} bins in {:.1f} s".format(n, n, sim.n_bins, t_sim), file=sys.stderr, flush=True)
     torch.zeros(1, device="cuda")
+    import contextlib
+    fit_stdout = contextlib.redirect_stdout(sys.stderr)          # the fit's own prints (convergence lines)
+    fit_stdout.__enter__()
     if args.config == "c2":
         from scdna_replication_tools_amd.infer_scRT import scRT
         t0 = time.perf_counter()
@@ -65,6 +68,7 @@ def main():
         cn_s_out, supp_s, cn_g1_out, supp_g1 = m.run_pert_model()
         clusters_ok = None
     print("fit done: {}".format(m.timings), file=sys.stderr, flush=True)
+    fit_stdout.__exit__(None, None, None)
     acc_cn = float((cn_s_out["model_cn_state"] == cn_s_out["true_somatic_cn"]).mean())
     acc_rep = float((cn_s_out["model_rep_state"] == cn_s_out["true_rep"]).mean())
     tm = m.timings

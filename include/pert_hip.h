@@ -145,7 +145,9 @@ typedef struct {
 int pert_make_layout(int32_t L, int32_t N, int32_t K1, int32_t n_libs, pert_layout* out);
 
 /* Workspace element counts for cell_part (float), bin_part (float), blk_part (double),
- * cellblk_part (double) at bins_per_tile (0 = default). */
+ * cellblk_part (double) at bins_per_tile (0 = default).  cellblk_part must be
+ * zero-initialised once: its last element holds pert_finalize's arrival counter, which
+ * every finalize launch leaves at zero again. */
 int pert_workspace_sizes(int32_t kind, int32_t L, int32_t N, int32_t K1, int32_t n_libs,
                          int32_t bins_per_tile, int64_t* n_cell_part, int64_t* n_bin_part,
                          int64_t* n_blk_part, int64_t* n_cellblk_part);
@@ -168,7 +170,8 @@ int pert_enum_pass(const pert_problem* prob, pert_state* st, const pert_adam_hpa
 int pert_obs_pass(const pert_problem* prob, pert_state* st, hipStream_t stream);
 
 /* Reductions of the pass partials + priors of the non-enumerated sites (pert_model.py:553-603)
- * -> grad_cell (local) and grad_shared (local partial sums incl. the loss in slot n_shared). */
+ * -> grad_cell (local) and grad_shared (local partial sums incl. the loss in slot n_shared).
+ * One launch: its last workgroup to finish adds the global sums. */
 int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream);
 
 /* Adam (torch.optim.Adam semantics, betas (0.8, 0.99)) on the packed params with

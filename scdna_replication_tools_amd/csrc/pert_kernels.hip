@@ -5,8 +5,8 @@
 //   enum_kernel / obs_kernel   one pass over every (bin, cell): forward, analytic backward,
 //                              fused Adam on the (L, P, N) pi logits, reduction partials
 //   finalize_kernel            per-cell sums + u / betas / tau priors (:589-603),
-//                              per-bin sums for rho (:572-574)
-//   scalar_kernel              global sums (loss, a, beta_stds, lambda, beta_means)
+//                              per-bin sums for rho (:572-574), and in its last block
+//                              the global sums (loss, a, beta_stds, lambda, beta_means)
 //   adam_kernel                Adam on the packed non-pi params
 // All reductions are fixed-order (no float atomics), so a rerun is bit-identical.
 //
@@ -90,7 +90,6 @@ __global__ void __launch_bounds__(kBlock, 2) enum_kernel(pert_problem pr, pert_s
   const pert_layout lay = st.lay;
 
   __shared__ float s_bin[kWaves][kMaxLT];
-  __shared__ double s_red[kWaves];
 
   const float a_val = frozen ? pr.a_fixed : fexp(st.params[lay.off_a]);
   const float c0 = (1.0f - pr.lamb) / pr.lamb;
@@ -252,14 +251,14 @@ __global__ void __launch_bounds__(kBlock, 2) enum_kernel(pert_problem pr, pert_s
       if (k < K1) cp[(size_t)k * N] = acc[k];
     cp[(size_t)K1 * N] = accT;
   }
-  const double bl = block_sum_d((double)loss, s_red);
-  const double bga = block_sum_d((double)ga, s_red);
-  if (tid == 0) {
-    double* bp = st.blk_part + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlkSlots;
+  // ELBO and d/da sums of each 64-cell wave: blk_part[bt][ldn/64] (read by the finalize
+  // block of that cell tile)
+  const double bl = wave_sum_d((double)loss);
+  const double bga = wave_sum_d((double)ga);
+  if (lane == 0) {
+    double* bp = st.blk_part + ((size_t)blockIdx.y * (ldn / 64) + (n >> 6)) * kBlkSlots;
     bp[0] = bl;
     bp[1] = bga;
-    bp[2] = 0.0;
-    bp[3] = 0.0;
   }
 }
 
@@ -533,14 +532,14 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
       if (k < K1) cp[(size_t)k * N] = acc[k];
     cp[(size_t)K1 * N] = accT;
   }
+  // the wave's ELBO and d/da sums: blk_part[bt][ldn/64] (read by the finalize block of
+  // this cell tile)
   const double bl = wave_sum_d((double)loss);
   const double bga = wave_sum_d((double)ga);
   if (lane == 0) {
-    double* bp = st.blk_part + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlkSlots;
+    double* bp = st.blk_part + ((size_t)blockIdx.y * (ldn / 64) + wt) * kBlkSlots;
     bp[0] = bl;
     bp[1] = bga;
-    bp[2] = 0.0;
-    bp[3] = 0.0;
   }
 }
 
@@ -685,90 +684,114 @@ __global__ void __launch_bounds__(kBlock) obs_kernel(pert_problem pr, pert_state
 }
 
 // ------------------------------------------------------------------------------------------
-// Per-cell and per-bin reductions + priors of the non-enumerated sites, one launch.
-// 1024-thread workgroups = 64 items (lanes) x 16 groups (waves).  Blocks [0, n_cblk) take
-// 64 cells each: group g sums the per-cell partials [n_bt][K1+1][N] of bin tiles g, g+16,
-// ... (independent loads, kFinU tiles in flight per thread), the 16 group sums are added in
-// fixed order through LDS, and wave 0 applies the priors.  Blocks [n_cblk, n_cblk+n_lblk)
-// take 64 bins each and sum bin_part [n_ct][L] the same way.  Every item is reduced in one
-// memory round trip, so the launch stays short when a small shard has many bin tiles.
+// Per-cell and per-bin reductions + priors of the non-enumerated sites + the global sums,
+// one launch.  1024-thread workgroups = 64 items (lanes) x 16 groups (waves).  Blocks
+// [0, n_cblk) take 64 cells each: group g sums the per-cell partials [n_bt][CS][N] of bin
+// tiles g, g+16, ... (independent loads, kFinU tiles in flight per thread), the 16 group
+// sums are added in fixed order through LDS, and wave 0 applies the priors.  Blocks
+// [n_cblk, n_cblk+n_lblk) take 64 bins each and sum bin_part [n_ct][L] the same way.  Every
+// item is reduced in one memory round trip, so the launch stays short when a small shard
+// has many bin tiles.  The last block to finish (arrival counter after the cell-block
+// partials, zeroed again by that block) adds the global sums -- the former separate
+// single-workgroup launch, now in the tail of this one.
+//
+// The pass partials: per cell and bin tile the K1 GC-feature sums and the tau sum
+// (cell_part [n_bt][K1+1][N]); the enumerated passes store each wave's ELBO and d/da sums
+// in blk_part [n_bt][ldn/64] (summed by the cell block of that tile), the observed pass
+// (step 1) each workgroup's ELBO / d/da / lambda sums (summed by the last block).
 constexpr int kFinBlock = 1024;
 constexpr int kFinG = kFinBlock / 64;
+__host__ __device__ constexpr int fin_slots(int n_libs, int K1) { return 2 * n_libs * K1 + 2; }
+
+// ---- per-bin: d(-ELBO)/dz_rho   (rho ~ Beta(1,1) has zero log density, :574)
+__device__ __forceinline__ void fin_bins(const pert_problem& pr, const pert_state& st, int lb, int n_ct,
+                                         double (*s_g)[64]) {
+  constexpr int kFinU = 4;
+  const int tid = threadIdx.x, lane = tid & 63, grp = tid >> 6;
+  const int L = pr.L;
+  const pert_layout lay = st.lay;
+  const int l = lb * 64 + lane;
+  const bool on = l < L && pr.kind != PERT_KIND_STEP3;
+  double s = 0.0;
+  if (on) {
+    const float* __restrict__ bp = st.bin_part;
+    for (int c0 = grp; c0 < n_ct; c0 += kFinG * kFinU) {
+      float v[kFinU];
+#pragma unroll
+      for (int u = 0; u < kFinU; ++u) {
+        const int ct = c0 + u * kFinG;
+        v[u] = ct < n_ct ? bp[(size_t)ct * L + l] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < kFinU; ++u) s += (double)v[u];
+    }
+  }
+  s_g[grp][lane] = s;
+  __syncthreads();
+  if (grp != 0 || l >= L) return;
+  if (pr.kind == PERT_KIND_STEP3) { st.grad_shared[lay.off_rho + l] = 0.0; return; }
+  double tot = 0.0;
+#pragma unroll
+  for (int g = 0; g < kFinG; ++g) tot += s_g[g][lane];
+  const float a_val = fexp(st.params[lay.off_a]);
+  float dmask;
+  clipped_sigmoid(st.params[lay.off_rho + l], &dmask);
+  // dE/drho = -a sum_n gt ;  loss gradient = +a sum gt * drho/dz
+  st.grad_shared[lay.off_rho + l] = (double)a_val * tot * (double)dmask;
+}
+
+// ---- per-cell: data sums over bin tiles + u / beta / tau priors -> grad_cell, and the
+// block's per-library beta_stds / beta_means sums, ELBO and d/da into cellblk_part
 template <int K1T>
-__global__ void __launch_bounds__(kFinBlock) finalize_kernel(pert_problem pr, pert_state st,
-                                                             int n_cblk, int n_bt, int n_ct) {
-  constexpr int kFinU = K1T <= 5 ? 4 : 2;    // bin tiles in flight per thread
-  if (loop_stopped(st)) return;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, grp = tid >> 6;
-  const int N = pr.N, K1 = (K1T == PERT_MAX_K1) ? pr.K1 : K1T, L = pr.L, nl = pr.n_libs;
+__device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_state& st, int cb, int n_bt,
+                                          double (*s_g)[64]) {
+  constexpr int kCS = K1T + 1;
+  constexpr int kFinU = K1T <= 5 ? 4 : 1;       // bin tiles in flight per thread
+  const int tid = threadIdx.x, lane = tid & 63, grp = tid >> 6;
+  const int N = pr.N, K1 = (K1T == PERT_MAX_K1) ? pr.K1 : K1T, nl = pr.n_libs;
   const pert_layout lay = st.lay;
   const bool step1 = pr.kind == PERT_KIND_STEP1;
-  __shared__ double s_g[kFinG][64];
-
-  if ((int)blockIdx.x >= n_cblk) {
-    // ---- per-bin: d(-ELBO)/dz_rho   (rho ~ Beta(1,1) has zero log density, :574)
-    const int l = (blockIdx.x - n_cblk) * 64 + lane;
-    const bool on = l < L && pr.kind != PERT_KIND_STEP3;
-    double s = 0.0;
-    if (on) {
-      const float* __restrict__ bp = st.bin_part;
-      for (int c0 = grp; c0 < n_ct; c0 += kFinG * kFinU) {
-        float v[kFinU];
-#pragma unroll
-        for (int u = 0; u < kFinU; ++u) {
-          const int ct = c0 + u * kFinG;
-          v[u] = ct < n_ct ? bp[(size_t)ct * L + l] : 0.0f;
-        }
-#pragma unroll
-        for (int u = 0; u < kFinU; ++u) s += (double)v[u];
-      }
-    }
-    s_g[grp][lane] = s;
-    __syncthreads();
-    if (grp != 0 || l >= L) return;
-    if (pr.kind == PERT_KIND_STEP3) { st.grad_shared[lay.off_rho + l] = 0.0; return; }
-    double tot = 0.0;
-#pragma unroll
-    for (int g = 0; g < kFinG; ++g) tot += s_g[g][lane];
-    const float a_val = fexp(st.params[lay.off_a]);
-    float dmask;
-    clipped_sigmoid(st.params[lay.off_rho + l], &dmask);
-    // dE/drho = -a sum_n gt ;  loss gradient = +a sum gt * drho/dz
-    st.grad_shared[lay.off_rho + l] = (double)a_val * tot * (double)dmask;
-    return;
-  }
-
-  // ---- per-cell
-  const int n = blockIdx.x * 64 + lane;
+  const int CS = K1 + 1;
+  const int n = cb * 64 + lane;
   const bool in_range = n < N;
-  double A[K1T + 1];
+  // the enumerated pass's ELBO / d/da sums of this cell tile, one bin tile per thread
+  // (issued first: independent of the cell partials below)
+  double wl = 0.0, wa = 0.0;
+  if (!step1) {
+    const size_t stride = (size_t)(pr.ldn / 64) * kBlkSlots;
+    for (int bt = tid; bt < n_bt; bt += kFinBlock) {
+      const double* bp = st.blk_part + (size_t)bt * stride + (size_t)cb * kBlkSlots;
+      wl += bp[0];
+      wa += bp[1];
+    }
+  }
+  double A[kCS];
 #pragma unroll
-  for (int k = 0; k <= K1T; ++k) A[k] = 0.0;
+  for (int k = 0; k < kCS; ++k) A[k] = 0.0;
   if (in_range) {
     const float* __restrict__ cp = st.cell_part;
-    const size_t tstride = (size_t)(K1 + 1) * N;
+    const size_t tstride = (size_t)CS * N;
     for (int b0 = grp; b0 < n_bt; b0 += kFinG * kFinU) {
-      float v[kFinU][K1T + 1];
+      float v[kFinU][kCS];
 #pragma unroll
       for (int u = 0; u < kFinU; ++u) {
         const int bt = b0 + u * kFinG;
 #pragma unroll
-        for (int k = 0; k <= K1T; ++k)
-          v[u][k] = (bt < n_bt && k <= K1) ? cp[(size_t)bt * tstride + (size_t)k * N + n] : 0.0f;
+        for (int k = 0; k < kCS; ++k)
+          v[u][k] = (bt < n_bt && k < CS) ? cp[(size_t)bt * tstride + (size_t)k * N + n] : 0.0f;
       }
 #pragma unroll
       for (int u = 0; u < kFinU; ++u)
 #pragma unroll
-        for (int k = 0; k <= K1T; ++k) A[k] += (double)v[u][k];
+        for (int k = 0; k < kCS; ++k) A[k] += (double)v[u][k];
     }
   }
   // fixed-order sum of the 16 groups, one state slot at a time (wave 0 keeps the totals)
-  double T[K1T + 1];
+  double T[kCS];
 #pragma unroll
-  for (int k = 0; k <= K1T; ++k) {
+  for (int k = 0; k < kCS; ++k) {
     T[k] = 0.0;
-    if (k > K1) continue;
+    if (k >= CS) continue;
     s_g[grp][lane] = A[k];
     __syncthreads();
     if (grp == 0) {
@@ -779,7 +802,15 @@ __global__ void __launch_bounds__(kFinBlock) finalize_kernel(pert_problem pr, pe
     }
     __syncthreads();
   }
+  // fixed-order block sum of the tile's ELBO / d/da sums (wave sums, then the 16 waves)
+  wl = wave_sum_d(wl);
+  wa = wave_sum_d(wa);
+  if (lane == 0) { s_g[grp][0] = wl; s_g[grp][1] = wa; }
+  __syncthreads();
   if (grp != 0) return;
+  double tile_l = 0.0, tile_a = 0.0;
+#pragma unroll
+  for (int g = 0; g < kFinG; ++g) { tile_l += s_g[g][0]; tile_a += s_g[g][1]; }
 
   const bool valid = in_range;
   float lam = pr.lamb;
@@ -798,7 +829,7 @@ __global__ void __launch_bounds__(kFinBlock) finalize_kernel(pert_problem pr, pe
 #pragma unroll
     for (int k = 0; k < K1T; ++k) Ak[k] = 0.0;
 #pragma unroll
-    for (int k = 0; k <= K1T; ++k) {
+    for (int k = 0; k < kCS; ++k) {
       if (k < K1) Ak[k] = T[k];
       if (k == K1) Tt = T[k];
     }
@@ -848,10 +879,10 @@ __global__ void __launch_bounds__(kFinBlock) finalize_kernel(pert_problem pr, pe
       if (k < K1) gc[lay.off_beta + k * N + n] = -dB[k];
     gc[lay.off_tau + n] = -dTau * dtau_dz;
   }
-  // per-library sums for beta_stds (and beta_means in step 1), plus the prior log densities:
+  // per-library sums for beta_stds (and beta_means in step 1), the ELBO and d/da:
   // wave 0 holds every value, one wave reduction per slot, fixed order
-  const int nslot = 2 * nl * K1 + 1;
-  double* out = st.cellblk_part + (size_t)blockIdx.x * nslot;
+  const int nslot = fin_slots(nl, K1);
+  double* out = st.cellblk_part + (size_t)cb * nslot;
   for (int sl = 0; sl < nslot; ++sl) {
     double val;
     if (sl < 2 * nl * K1) {
@@ -864,42 +895,28 @@ __global__ void __launch_bounds__(kFinBlock) finalize_kernel(pert_problem pr, pe
         if (kk == k) fv = half == 0 ? dzbs[kk] : dbm[kk];
       val = mine ? (double)fv : 0.0;
     } else {
-      val = lp;
+      val = sl == 2 * nl * K1 ? lp : 0.0;
     }
     val = wave_sum_d(val);
-    if (lane == 0) out[sl] = val;
+    if (lane == 0) out[sl] = val + (sl == 2 * nl * K1 ? tile_l : (sl == 2 * nl * K1 + 1 ? tile_a : 0.0));
   }
 }
 
-// Global sums: one 1024-thread workgroup, fixed order.
-constexpr int kScalarBlock = 1024;
-__device__ __forceinline__ double block_sum_d1024(double v, double* sm) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  v = wave_sum_d(v);
-  __syncthreads();
-  if (lane == 0) sm[wave] = v;
-  __syncthreads();
-  double t = 0.0;
-#pragma unroll
-  for (int w = 0; w < kScalarBlock / 64; ++w) t += sm[w];
-  return t;
-}
-
-__global__ void __launch_bounds__(kScalarBlock) scalar_kernel(pert_problem pr, pert_state st, int n_blk,
-                                                              int n_cblk) {
-  if (loop_stopped(st)) return;
+// ---- global sums (the last block): loss, a, beta_stds, lambda, beta_means; fixed order
+__device__ void fin_global(const pert_problem& pr, const pert_state& st, int n_blk, int n_cblk) {
   const int tid = threadIdx.x;
   const int K1 = pr.K1, nl = pr.n_libs;
   const pert_layout lay = st.lay;
   const int kind = pr.kind;
-  constexpr int kSW = kScalarBlock / 64;
+  constexpr int kSW = kFinBlock / 64;
   __shared__ double s_red4[kSW][kBlkSlots];
   __shared__ double s_slot[64];
   const int lane = tid & 63, wave = tid >> 6;
-  // (1) the enum/obs block partials: all 1024 threads, double4 per block, one LDS round
+  // (1) the observed pass's workgroup partials (step 1; none for the enumerated passes):
+  //     all 1024 threads, double4 per workgroup, one LDS round
   double v[kBlkSlots] = {0.0, 0.0, 0.0, 0.0};
   const double4* bp4 = reinterpret_cast<const double4*>(st.blk_part);
-  for (int b = tid; b < n_blk; b += kScalarBlock) {
+  for (int b = tid; b < n_blk; b += kFinBlock) {
     const double4 q = bp4[b];
     v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
   }
@@ -909,8 +926,8 @@ __global__ void __launch_bounds__(kScalarBlock) scalar_kernel(pert_problem pr, p
 #pragma unroll
     for (int j = 0; j < kBlkSlots; ++j) s_red4[wave][j] = v[j];
   }
-  // (2) the finalize cell-block partials: one wave per slot (fixed order)
-  const int nslot = 2 * nl * K1 + 1;
+  // (2) the cell-block partials: one wave per slot (fixed order)
+  const int nslot = fin_slots(nl, K1);
   for (int sl = wave; sl < nslot; sl += kSW) {
     double acc = 0.0;
     for (int b = lane; b < n_cblk; b += 64) acc += st.cellblk_part[(size_t)b * nslot + sl];
@@ -940,11 +957,12 @@ __global__ void __launch_bounds__(kScalarBlock) scalar_kernel(pert_problem pr, p
       } else {
         st.grad_shared[lay.off_bmeans + j] = 0.0;
       }
-    } else {
+    } else if (sl == 2 * nl * K1) {
       elbo += S;
+    } else {
+      tot[1] += S;
     }
   }
-  if (tid != 0) return;
   // global sites
   if (kind != PERT_KIND_STEP3) {
     const double a = exp((double)st.params[lay.off_a]);
@@ -986,6 +1004,30 @@ __global__ void __launch_bounds__(kScalarBlock) scalar_kernel(pert_problem pr, p
     }
   }
   st.grad_shared[lay.n_shared] = -elbo;                     // local loss (host adds constants)
+}
+
+template <int K1T>
+__global__ void __launch_bounds__(kFinBlock) finalize_kernel(pert_problem pr, pert_state st, int n_cblk,
+                                                             int n_bt, int n_ct, int n_blk) {
+  if (loop_stopped(st)) return;
+  __shared__ double s_g[kFinG][64];
+  __shared__ int s_last;
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x >= n_cblk) fin_bins(pr, st, blockIdx.x - n_cblk, n_ct, s_g);
+  else fin_cells<K1T>(pr, st, blockIdx.x, n_bt, s_g);
+  // Wave 0 wrote this block's outputs: publish them (agent-scope release), then count the
+  // block in.  The last block to arrive acquires and runs the global sums, then re-arms
+  // the counter for the next launch.
+  if (tid < 64) __threadfence();
+  __syncthreads();
+  unsigned int* arrivals = reinterpret_cast<unsigned int*>(
+      st.cellblk_part + (size_t)n_cblk * fin_slots(pr.n_libs, pr.K1));
+  if (tid == 0) s_last = atomicAdd(arrivals, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  fin_global(pr, st, n_blk, n_cblk);
+  if (tid == 0) atomicExch(arrivals, 0u);
 }
 
 // Loss of iteration st.step and the reference's stopping rule, evaluated by one thread after
@@ -1188,7 +1230,9 @@ int pert_workspace_sizes(int32_t kind, int32_t L, int32_t N, int32_t K1, int32_t
   if (n_cell_part) *n_cell_part = n_bt * (K1 + 1) * (int64_t)N;
   if (n_bin_part) *n_bin_part = n_ct * (int64_t)L;
   if (n_blk_part) *n_blk_part = n_bt * n_ct * kBlkSlots;
-  if (n_cellblk_part) *n_cellblk_part = ((N + 63) / 64) * (2 * (int64_t)n_libs * K1 + 1);
+  // the cell-block partials, then one element whose first 4 bytes are the finalize
+  // launch's arrival counter (zero-initialised by the caller, re-armed by every launch)
+  if (n_cellblk_part) *n_cellblk_part = ((N + 63) / 64) * (int64_t)fin_slots(n_libs, K1) + 1;
   return PERT_OK;
 }
 
@@ -1203,8 +1247,11 @@ int pert_auto_bins_per_tile(const pert_problem* prob, int32_t variant, int32_t* 
   if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return hip_status(e);
   // Each resident wave runs one tile (a prologue of about kTilePrologue bins plus lt bins);
-  // the pass takes ceil(tiles / slots) such rounds.  Pick the lt with the least predicted
-  // time, the longer tile on a tie.
+  // the pass takes ceil(tiles / slots) such rounds, and the last round ends with a tail in
+  // which the slowest waves finish their tiles: wave exits spread over about 1/8 of a tile
+  // (tools/wave_timeline.py, one-round launch: exits 453-551 us for 56-bin tiles).  Pick
+  // the lt with the least predicted time (in 1/8 bins), the longer tile on a tie.  At 1,250
+  // cells this takes two rounds of 27 bins over one of 54 (-3 % kernel, tools/lt_sweep.sh).
   constexpr int kTilePrologue = 2;
   const long n_ct = (prob->N + 63) / 64;
   long best = -1;
@@ -1215,7 +1262,7 @@ int pert_auto_bins_per_tile(const pert_problem* prob, int32_t variant, int32_t* 
     const long slots = (long)ncu * occ;
     const long tiles = n_ct * ((prob->L + lt - 1) / lt);
     const long rounds = (tiles + slots - 1) / slots;
-    const long cost = rounds * (lt + kTilePrologue);
+    const long cost = (8 * rounds + 1) * (lt + kTilePrologue);
     if (best < 0 || cost < best) { best = cost; best_lt = lt; }
   }
   *out = best_lt;
@@ -1264,16 +1311,14 @@ int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream) 
   const int n_bt = (prob->L + lt - 1) / lt;
   const int n_lblk = (prob->L + 63) / 64;
   const int n_cblk = (prob->N + 63) / 64;
+  const int n_blk = prob->kind == PERT_KIND_STEP1 ? n_bt * n_ct : 0;   // observed pass only
+  if (fin_slots(prob->n_libs, prob->K1) > 64) return PERT_E_ARG;         // fin_global's slot table
   if (prob->K1 == 5)
     hipLaunchKernelGGL(finalize_kernel<5>, dim3(n_cblk + n_lblk), dim3(kFinBlock), 0, stream, *prob, s2, n_cblk,
-                       n_bt, n_ct);
+                       n_bt, n_ct, n_blk);
   else
     hipLaunchKernelGGL(finalize_kernel<PERT_MAX_K1>, dim3(n_cblk + n_lblk), dim3(kFinBlock), 0, stream, *prob, s2,
-                       n_cblk, n_bt, n_ct);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return hip_status(e);
-  if (2 * prob->n_libs * prob->K1 + 1 > 64) return PERT_E_ARG;       // scalar_kernel's slot table
-  hipLaunchKernelGGL(scalar_kernel, dim3(1), dim3(kScalarBlock), 0, stream, *prob, s2, n_bt * n_ct, n_cblk);
+                       n_cblk, n_bt, n_ct, n_blk);
   return hip_status(hipGetLastError());
 }
 

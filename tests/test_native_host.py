@@ -54,7 +54,8 @@ def test_layout_and_workspace(nat):
     assert lay.n_shared == 100 + 2 + 2 * 2 * 5
     assert lay.off_tau + 37 == lay.n_params
     ncp, nbp, nblk, ncb = nat.workspace_sizes(2, 100, 37, 5, 2, 32)
-    assert ncp == 4 * 6 * 37 and nbp == (256 // 64) * 100 and ncb == ((37 + 63) // 64) * (2 * 2 * 5 + 1)
+    assert ncp == 4 * (5 + 1) * 37 and nbp == (256 // 64) * 100 and ncb == ((37 + 63) // 64) * (2 * 2 * 5 + 2) + 1
+    assert nat.workspace_sizes(1, 100, 37, 5, 2, 32)[0] == 4 * (5 + 1) * 37
     with pytest.raises(ValueError):
         nat.make_layout(0, 1, 5, 1)
 

@@ -47,3 +47,10 @@ for x in range(8):
     m = xcc == x
     if m.any():
         print("xcc {} waves {} exit p50 {:.1f} p100 {:.1f} mean dur {:.1f}".format(x, m.sum(), np.median(ex[m]), ex[m].max(), dur[m].mean()))
+first_round = ent < 20.0
+if (~first_round).any():
+    print("wave dur first round (entry < 20 us) pct:", q(dur[first_round]))
+    print("wave dur later rounds pct            :", q(dur[~first_round]))
+    mid = (ent > 0.3 * span) & (ex < 0.7 * span)
+    if mid.any():
+        print("wave dur mid-kernel pct              :", q(dur[mid]))

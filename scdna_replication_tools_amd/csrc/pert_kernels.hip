@@ -705,13 +705,19 @@ __host__ __device__ constexpr int fin_slots(int n_libs, int K1) { return 2 * n_l
 
 // ---- per-bin: d(-ELBO)/dz_rho   (rho ~ Beta(1,1) has zero log density, :574)
 __device__ __forceinline__ void fin_bins(const pert_problem& pr, const pert_state& st, int lb, int n_ct,
-                                         double (*s_g)[64]) {
+                                         bool stopped, double (*s_g)[64]) {
   constexpr int kFinU = 4;
   const int tid = threadIdx.x, lane = tid & 63, grp = tid >> 6;
   const int L = pr.L;
   const pert_layout lay = st.lay;
   const int l = lb * 64 + lane;
   const bool on = l < L && pr.kind != PERT_KIND_STEP3;
+  // wave 0's parameters, loaded before the partials so the two round trips overlap
+  float a_z = 0.0f, rho_z = 0.0f;
+  if (grp == 0 && on) {
+    a_z = st.params[lay.off_a];
+    rho_z = st.params[lay.off_rho + l];
+  }
   double s = 0.0;
   if (on) {
     const float* __restrict__ bp = st.bin_part;
@@ -728,23 +734,26 @@ __device__ __forceinline__ void fin_bins(const pert_problem& pr, const pert_stat
   }
   s_g[grp][lane] = s;
   __syncthreads();
-  if (grp != 0 || l >= L) return;
+  if (stopped || grp != 0 || l >= L) return;
   if (pr.kind == PERT_KIND_STEP3) { st.grad_shared[lay.off_rho + l] = 0.0; return; }
   double tot = 0.0;
 #pragma unroll
   for (int g = 0; g < kFinG; ++g) tot += s_g[g][lane];
-  const float a_val = fexp(st.params[lay.off_a]);
+  const float a_val = fexp(a_z);
   float dmask;
-  clipped_sigmoid(st.params[lay.off_rho + l], &dmask);
+  clipped_sigmoid(rho_z, &dmask);
   // dE/drho = -a sum_n gt ;  loss gradient = +a sum gt * drho/dz
   st.grad_shared[lay.off_rho + l] = (double)a_val * tot * (double)dmask;
 }
 
 // ---- per-cell: data sums over bin tiles + u / beta / tau priors -> grad_cell, and the
-// block's per-library beta_stds / beta_means sums, ELBO and d/da into cellblk_part
+// block's per-library beta_stds / beta_means sums, ELBO and d/da into cellblk_part.
+// Everything wave 0 needs besides the sums (its cells' parameters, the per-library prior
+// table in LDS, the tile's ELBO / d/da partials) is requested before the partial loop.
+constexpr int kFinLibSlots = 32;                 // n_libs * K1 <= 31 (fin_slots <= 64)
 template <int K1T>
 __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_state& st, int cb, int n_bt,
-                                          double (*s_g)[64]) {
+                                          bool stopped, double (*s_g)[64]) {
   constexpr int kCS = K1T + 1;
   constexpr int kFinU = K1T <= 5 ? 4 : 1;       // bin tiles in flight per thread
   const int tid = threadIdx.x, lane = tid & 63, grp = tid >> 6;
@@ -754,16 +763,36 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
   const int CS = K1 + 1;
   const int n = cb * 64 + lane;
   const bool in_range = n < N;
+  __shared__ float s_bsd[kFinLibSlots], s_bmn[kFinLibSlots];
+  __shared__ double s_cs[kCS][kFinG][64];
+  // per-library prior table: beta_stds (constrained) and beta_means
+  if (tid < nl * K1) {
+    s_bsd[tid] = fexp(st.params[lay.off_bstds + tid]);
+    s_bmn[tid] = step1 ? st.params[lay.off_bmeans + tid] : pr.beta_means[tid];
+  }
+  // wave 0: its cells' parameters
+  float u = 0.0f, tau_z = 0.0f, mean_x = 1.0f, ploidy = 1.0f;
+  int lib = 0;
+  float bz[K1T];
+#pragma unroll
+  for (int k = 0; k < K1T; ++k) bz[k] = 0.0f;
+  if (grp == 0 && in_range) {
+    u = st.params[lay.off_u + n];
+    tau_z = st.params[lay.off_tau + n];
+    lib = pr.libs[n];
+    mean_x = pr.mean_reads[n];
+    ploidy = pr.ploidy[n];
+#pragma unroll
+    for (int k = 0; k < K1T; ++k)
+      if (k < K1) bz[k] = st.params[lay.off_beta + k * N + n];
+  }
   // the enumerated pass's ELBO / d/da sums of this cell tile, one bin tile per thread
-  // (issued first: independent of the cell partials below)
   double wl = 0.0, wa = 0.0;
-  if (!step1) {
-    const size_t stride = (size_t)(pr.ldn / 64) * kBlkSlots;
-    for (int bt = tid; bt < n_bt; bt += kFinBlock) {
-      const double* bp = st.blk_part + (size_t)bt * stride + (size_t)cb * kBlkSlots;
-      wl += bp[0];
-      wa += bp[1];
-    }
+  const size_t bstride = (size_t)(pr.ldn / 64) * kBlkSlots;
+  if (!step1 && tid < n_bt) {
+    const double* bp = st.blk_part + (size_t)tid * bstride + (size_t)cb * kBlkSlots;
+    wl = bp[0];
+    wa = bp[1];
   }
   double A[kCS];
 #pragma unroll
@@ -786,28 +815,32 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
         for (int k = 0; k < kCS; ++k) A[k] += (double)v[u][k];
     }
   }
-  // fixed-order sum of the 16 groups, one state slot at a time (wave 0 keeps the totals)
-  double T[kCS];
-#pragma unroll
-  for (int k = 0; k < kCS; ++k) {
-    T[k] = 0.0;
-    if (k >= CS) continue;
-    s_g[grp][lane] = A[k];
-    __syncthreads();
-    if (grp == 0) {
-      double t = 0.0;
-#pragma unroll
-      for (int g = 0; g < kFinG; ++g) t += s_g[g][lane];
-      T[k] = t;
+  if (!step1) {
+    for (int bt = tid + kFinBlock; bt < n_bt; bt += kFinBlock) {
+      const double* bp = st.blk_part + (size_t)bt * bstride + (size_t)cb * kBlkSlots;
+      wl += bp[0];
+      wa += bp[1];
     }
-    __syncthreads();
   }
-  // fixed-order block sum of the tile's ELBO / d/da sums (wave sums, then the 16 waves)
+  // fixed-order sums of the 16 groups: every slot through LDS in one round
+#pragma unroll
+  for (int k = 0; k < kCS; ++k)
+    if (k < CS) s_cs[k][grp][lane] = A[k];
   wl = wave_sum_d(wl);
   wa = wave_sum_d(wa);
   if (lane == 0) { s_g[grp][0] = wl; s_g[grp][1] = wa; }
   __syncthreads();
-  if (grp != 0) return;
+  if (stopped || grp != 0) return;
+  double T[kCS];
+#pragma unroll
+  for (int k = 0; k < kCS; ++k) {
+    double t = 0.0;
+    if (k < CS) {
+#pragma unroll 4
+      for (int g = 0; g < kFinG; ++g) t += s_cs[k][g][lane];
+    }
+    T[k] = t;
+  }
   double tile_l = 0.0, tile_a = 0.0;
 #pragma unroll
   for (int g = 0; g < kFinG; ++g) { tile_l += s_g[g][0]; tile_a += s_g[g][1]; }
@@ -821,7 +854,6 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
   const float c0 = (1.0f - lam) / lam;
   double lp = 0.0;
   float dzbs[K1T], dbm[K1T];
-  int lib = 0;
 #pragma unroll
   for (int k = 0; k < K1T; ++k) { dzbs[k] = 0.0f; dbm[k] = 0.0f; }
   if (valid) {
@@ -833,10 +865,8 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
       if (k < K1) Ak[k] = T[k];
       if (k == K1) Tt = T[k];
     }
-    const float u = st.params[lay.off_u + n];
     float dtau_dz;
-    const float tau = clipped_sigmoid(st.params[lay.off_tau + n], &dtau_dz);
-    lib = pr.libs[n];
+    const float tau = clipped_sigmoid(tau_z, &dtau_dz);
     // data terms: dE/du = c0 sum_l gD omega (intercept column of gcf is 1), dE/dbeta_k = u c0 sum gD omega g_k
     float dU = c0 * (float)Ak[K1 - 1];
     float dTau = (float)Tt;
@@ -845,7 +875,7 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
     for (int k = 0; k < K1T; ++k) dB[k] = (k < K1) ? u * c0 * (float)Ak[k] : 0.0f;
 
     // u ~ Normal(mu, mu/10), mu = mean(x) / ((1 + tau) ploidy)   (:597-600)
-    const float mu = pr.mean_reads[n] / ((1.0f + tau) * pr.ploidy[n]);
+    const float mu = mean_x / ((1.0f + tau) * ploidy);
     const float sg = mu / 10.0f;
     const float w = (u - mu) / sg;
     lp += (double)(-0.5f * w * w - logf(sg) - kHalfLog2PiF);
@@ -857,9 +887,9 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
 #pragma unroll
     for (int k = 0; k < K1T; ++k) {
       if (k >= K1) continue;
-      const float bsd = fexp(st.params[lay.off_bstds + lib * K1 + k]);
-      const float bmn = step1 ? st.params[lay.off_bmeans + lib * K1 + k] : pr.beta_means[lib * K1 + k];
-      const float b = st.params[lay.off_beta + k * N + n];
+      const float bsd = s_bsd[lib * K1 + k];
+      const float bmn = s_bmn[lib * K1 + k];
+      const float b = bz[k];
       const float wk = (b - bmn) / bsd;
       lp += (double)(-0.5f * wk * wk - logf(bsd) - kHalfLog2PiF);
       dB[k] += -wk / bsd;
@@ -1009,12 +1039,15 @@ __device__ void fin_global(const pert_problem& pr, const pert_state& st, int n_b
 template <int K1T>
 __global__ void __launch_bounds__(kFinBlock) finalize_kernel(pert_problem pr, pert_state st, int n_cblk,
                                                              int n_bt, int n_ct, int n_blk) {
-  if (loop_stopped(st)) return;
+  // the device loop's stop flag is read first but tested only before the first store, so
+  // its round trip overlaps the partial loads (a stopped launch writes nothing)
+  const bool stopped = loop_stopped(st);
   __shared__ double s_g[kFinG][64];
   __shared__ int s_last;
   const int tid = threadIdx.x;
-  if ((int)blockIdx.x >= n_cblk) fin_bins(pr, st, blockIdx.x - n_cblk, n_ct, s_g);
-  else fin_cells<K1T>(pr, st, blockIdx.x, n_bt, s_g);
+  if ((int)blockIdx.x >= n_cblk) fin_bins(pr, st, blockIdx.x - n_cblk, n_ct, stopped, s_g);
+  else fin_cells<K1T>(pr, st, blockIdx.x, n_bt, stopped, s_g);
+  if (stopped) return;
   // Wave 0 wrote this block's outputs: publish them (agent-scope release), then count the
   // block in.  The last block to arrive acquires and runs the global sums, then re-arms
   // the counter for the next launch.

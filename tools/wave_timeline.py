@@ -20,7 +20,7 @@ bm = np.zeros((1, 5)); bm[0, 3] = 0.5
 init = init_params(2, reads, np.zeros(cells, int), 1, 13, 4, ploidy=eta.argmax_states().mean(0),
                    t_init=np.clip(data["tau"].cpu().numpy(), 0.05, 0.95), beta_means=bm, seed=0)
 sh = PertShard(2, reads, data["gc"], np.zeros(cells, int), 1, 13, 4, init, eta=eta, lamb=0.75, beta_means=bm,
-               device=dev, variant=int(os.environ.get("VARIANT", "2")))
+               device=dev, variant=2, bins_per_tile=int(os.environ.get("LT", "0")))
 L = reads.shape[0]
 n_wg = (-(-cells // 64)) * (-(-L // sh.bins_per_tile))
 dbg = torch.zeros(n_wg * 4, dtype=torch.int64, device=dev)

@@ -350,19 +350,40 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
   // dependent global load after the forward pass
   float* s_tab = s_bc + LT * (K1 + 1);
   const bool etal = !kDecode && pr.n_codes * (P + 1) <= kEtaLdsFloats;
-  if (etal)
-    for (int i = lane; i < pr.n_codes * (P + 1); i += 64) s_tab[i] = pr.eta_table[i];
-  // per-bin constants of the tile: constrained rho and the GC features
-  for (int i = lane; i < (l1 - l0) * (K1 + 1); i += 64) {
-    const int lb = i / (K1 + 1), j = i - lb * (K1 + 1);
-    float v;
-    if (j == 0) {
+  // Tile prologue: every load below is unconditional (clamped index, masked store), so each
+  // group is one round trip instead of one guarded load + wait per loop trip.
+  if (etal) {
+    const int nt = pr.n_codes * (P + 1);
+    float tv[kEtaLdsFloats / 64];
+#pragma unroll
+    for (int r = 0; r < kEtaLdsFloats / 64; ++r) tv[r] = pr.eta_table[min(lane + 64 * r, nt - 1)];
+#pragma unroll
+    for (int r = 0; r < kEtaLdsFloats / 64; ++r)
+      if (lane + 64 * r < nt) s_tab[lane + 64 * r] = tv[r];
+  }
+  // per-bin constants of the tile: constrained rho (one bin per lane, LT <= 64) and the
+  // GC features (a contiguous run of nb * K1 floats of gcf)
+  {
+    const int nb = l1 - l0;
+    const int lr = l0 + min(lane, nb - 1);
+    const float zr = frozen ? pr.rho_fixed[lr] : params[lay.off_rho + lr];
+    const int ng = nb * K1;
+    const float* gsrc = pr.gcf + (size_t)l0 * K1;
+    float gv[PERT_MAX_K1];
+#pragma unroll
+    for (int r = 0; r < PERT_MAX_K1; ++r) gv[r] = gsrc[min(lane + 64 * r, ng - 1)];
+    if (lane < nb) {
       float dm;
-      v = frozen ? pr.rho_fixed[l0 + lb] : clipped_sigmoid(params[lay.off_rho + l0 + lb], &dm);
-    } else {
-      v = pr.gcf[(l0 + lb) * K1 + j - 1];
+      s_bc[lane * (K1 + 1)] = frozen ? zr : clipped_sigmoid(zr, &dm);
     }
-    s_bc[i] = v;
+#pragma unroll
+    for (int r = 0; r < PERT_MAX_K1; ++r) {
+      const int i = lane + 64 * r;
+      if (i < ng) {
+        const int lb = i / K1, j = i - lb * K1;
+        s_bc[lb * (K1 + 1) + 1 + j] = gv[r];
+      }
+    }
   }
   const float a_val = frozen ? pr.a_fixed : fexp(params[lay.off_a]);
   const float c0 = (1.0f - pr.lamb) / pr.lamb;
@@ -725,8 +746,11 @@ __device__ __forceinline__ void fin_bins(const pert_problem& pr, const pert_stat
       float v[kFinU];
 #pragma unroll
       for (int u = 0; u < kFinU; ++u) {
+        // clamped index, masked value: the loads stay unconditional, so they are all in
+        // flight together (a guarded load compiles to a branch with its own wait)
         const int ct = c0 + u * kFinG;
-        v[u] = ct < n_ct ? bp[(size_t)ct * L + l] : 0.0f;
+        const float x = bp[(size_t)min(ct, n_ct - 1) * L + l];
+        v[u] = ct < n_ct ? x : 0.0f;
       }
 #pragma unroll
       for (int u = 0; u < kFinU; ++u) s += (double)v[u];
@@ -805,9 +829,12 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
 #pragma unroll
       for (int u = 0; u < kFinU; ++u) {
         const int bt = b0 + u * kFinG;
+        const float* row = cp + (size_t)min(bt, n_bt - 1) * tstride + n;   // clamped, see fin_bins
 #pragma unroll
-        for (int k = 0; k < kCS; ++k)
-          v[u][k] = (bt < n_bt && k < CS) ? cp[(size_t)bt * tstride + (size_t)k * N + n] : 0.0f;
+        for (int k = 0; k < kCS; ++k) {
+          const float x = row[(size_t)min(k, CS - 1) * N];
+          v[u][k] = (bt < n_bt && k < CS) ? x : 0.0f;
+        }
       }
 #pragma unroll
       for (int u = 0; u < kFinU; ++u)

@@ -1,5 +1,6 @@
 #!/bin/bash
-# finalize attribution (diagnostic build ab/probe.so): PERT_FIN_PROBE=1 empty kernel before
+# finalize attribution. ab/probe.so = a build of pert_kernels.hip whose pert_finalize reads
+# PERT_FIN_PROBE (not kept in-tree): 1 = an empty kernel before
 # finalize, 2 = + only the per-bin blocks, 3 = + only the per-cell blocks
 set -o pipefail
 R=$(pwd)

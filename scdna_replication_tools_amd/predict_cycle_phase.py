@@ -34,7 +34,9 @@ def autocorr(data, min_lag: int = MIN_LAG, max_lag: int = MAX_LAG) -> float:
     n = x.size
     d = x - x.mean()
     c0 = (d * d).sum()
-    acorr = np.array([1.0] + [(d[:n - k] * d[k:]).sum() / c0 for k in range(1, max_lag + 1)])
+    # a constant series has c0 = 0: NaN, as statsmodels' acf returns (no warning)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        acorr = np.array([1.0] + [(d[:n - k] * d[k:]).sum() / c0 for k in range(1, max_lag + 1)])
     return float(np.mean(acorr[min_lag - 1:]))
 
 

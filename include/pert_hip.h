@@ -90,7 +90,7 @@ typedef struct {
   const float* ploidy;             /* [N] mean argmax eta (steps 2/3) or 2 (step 1) */
   float lamb;                      /* steps 2/3: fixed lambda from step 1 */
   float log1m_lam;                 /* log(1 - lamb) */
-  float sum_reads;                 /* step 1: sum of reads of this shard (d/dlam of x log lam) */
+  double sum_reads;                /* step 1: sum of reads of this shard (d/dlam of x log lam), fp64 */
   float a_fixed;                   /* step 3 */
   const float* beta_means;         /* steps 2/3 fixed [n_libs][K1] */
   const float* rho_fixed;          /* step 3 [L] constrained */

@@ -11,10 +11,11 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_void_p
 
 LIB_NAME = "libpert_hip.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+DEFAULT_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # A/B measurement hook: PERT_LIB names another build of the same ABI (e.g. a previous
-# kernel version compiled by tools/build_ab.sh); the product default is LIB_PATH.
-LIB_PATH = os.environ.get("PERT_LIB", LIB_PATH)
+# kernel version compiled by tools/build_ab.sh); the product default is the in-tree build,
+# whose provenance lib() checks.
+LIB_PATH = os.environ.get("PERT_LIB", DEFAULT_LIB_PATH)
 
 KIND_STEP1, KIND_STEP2, KIND_STEP3 = 1, 2, 3
 MODE_STEP, MODE_GRAD, MODE_DECODE = 0, 1, 2
@@ -46,7 +47,7 @@ class PertProblem(ctypes.Structure):
         ("reads", c_void_p), ("gcf", c_void_p), ("libs", c_void_p), ("eta_code", c_void_p),
         ("eta_table", c_void_p), ("cn_obs", c_void_p), ("rep_obs", c_void_p),
         ("mean_reads", c_void_p), ("ploidy", c_void_p),
-        ("lamb", c_float), ("log1m_lam", c_float), ("sum_reads", c_float), ("a_fixed", c_float),
+        ("lamb", c_float), ("log1m_lam", c_float), ("sum_reads", c_double), ("a_fixed", c_float),
         ("beta_means", c_void_p), ("rho_fixed", c_void_p),
     ]
 
@@ -74,11 +75,31 @@ _lib = None
 
 
 def lib():
-    """Load libpert_hip.so once; raise loudly if it is absent or incomplete."""
+    """Load libpert_hip.so once; raise loudly if it is absent, incomplete or stale (its
+    embedded source hash differs from the sources of this tree, build.source_hash())."""
     global _lib
     if _lib is None:
-        _lib = load(LIB_PATH)
+        handle = load(LIB_PATH)
+        check_provenance(handle)
+        _lib = handle
     return _lib
+
+
+def library_source_hash(handle) -> str:
+    v = handle.pert_version().decode()
+    return v.split("src=", 1)[1] if "src=" in v else ""
+
+
+def check_provenance(handle):
+    """The product library must be built from the sources beside it."""
+    from . import build
+    if os.path.abspath(LIB_PATH) != DEFAULT_LIB_PATH or not all(os.path.exists(d) for d in build.DEPS):
+        return                      # sources not shipped: nothing to compare against
+    want, got = build.source_hash(), library_source_hash(handle)
+    if got != want:
+        raise NativeLibraryError(
+            "{} is stale: built from sources {} but the tree's sources hash to {} (rebuild with "
+            "`python -m scdna_replication_tools_amd.build`)".format(LIB_PATH, got or "<unknown>", want))
 
 
 def load(path: str):

@@ -1,11 +1,20 @@
 """Build libpert_hip.so in-tree for gfx950 (hipcc, no JIT cache).
 
     python -m scdna_replication_tools_amd.build [--force] [--verbose]
+
+Provenance: the SHA-256 of the sources the library is compiled from (``SOURCES`` +
+headers, ``source_hash()``) is baked into the binary and returned by
+``pert_version()`` ("... src=<hash>").  ``build()`` rebuilds whenever the library's
+embedded hash differs from the tree's (not by file times), and ``_native.lib()``
+refuses a library whose hash does not match the sources next to it, so a stale
+binary shipped with the tree fails loudly instead of passing tests.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import os
+import re
 import subprocess
 import sys
 
@@ -15,6 +24,7 @@ SOURCES = [os.path.join(HERE, "csrc", "pert_kernels.hip")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", "pert_math.h"), os.path.join(ROOT, "include", "pert_hip.h")]
 OUT = os.path.join(HERE, "libpert_hip.so")
 ARCH = os.environ.get("PERT_OFFLOAD_ARCH", "gfx950")
+HASH_LEN = 16
 
 
 def hipcc() -> str:
@@ -24,17 +34,35 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+def source_hash() -> str:
+    """SHA-256 (first 16 hex digits) over the library's sources, in a fixed order."""
+    h = hashlib.sha256()
+    for d in DEPS:
+        h.update(os.path.basename(d).encode())
+        with open(d, "rb") as fh:
+            h.update(fh.read())
+    h.update(ARCH.encode())
+    return h.hexdigest()[:HASH_LEN]
+
+
+def embedded_hash(path: str = OUT):
+    """The source hash baked into a built library (read from its bytes; no load)."""
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as fh:
+        m = re.search(rb"pert_hip [0-9.]+ gfx950 src=([0-9a-f]{%d})" % HASH_LEN, fh.read())
+    return m.group(1).decode() if m else None
+
+
 def up_to_date() -> bool:
-    if not os.path.exists(OUT):
-        return False
-    t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(d) <= t for d in DEPS)
+    return embedded_hash(OUT) == source_hash()
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and up_to_date():
         return OUT
     cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-shared", "-fPIC",
+           "-DPERT_SOURCE_HASH=\"{}\"".format(source_hash()),
            "-I" + os.path.join(ROOT, "include"), *SOURCES, "-o", OUT + ".tmp"]
     if verbose:
         cmd.append("-Rpass-analysis=kernel-resource-usage")

@@ -774,7 +774,6 @@ __device__ __forceinline__ void fin_bins(const pert_problem& pr, const pert_stat
 // block's per-library beta_stds / beta_means sums, ELBO and d/da into cellblk_part.
 // Everything wave 0 needs besides the sums (its cells' parameters, the per-library prior
 // table in LDS, the tile's ELBO / d/da partials) is requested before the partial loop.
-constexpr int kFinLibSlots = 32;                 // n_libs * K1 <= 31 (fin_slots <= 64)
 template <int K1T>
 __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_state& st, int cb, int n_bt,
                                           bool stopped, double (*s_g)[64]) {
@@ -787,19 +786,14 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
   const int CS = K1 + 1;
   const int n = cb * 64 + lane;
   const bool in_range = n < N;
-  __shared__ float s_bsd[kFinLibSlots], s_bmn[kFinLibSlots];
   __shared__ double s_cs[kCS][kFinG][64];
-  // per-library prior table: beta_stds (constrained) and beta_means
-  if (tid < nl * K1) {
-    s_bsd[tid] = fexp(st.params[lay.off_bstds + tid]);
-    s_bmn[tid] = step1 ? st.params[lay.off_bmeans + tid] : pr.beta_means[tid];
-  }
-  // wave 0: its cells' parameters
+  // wave 0: its cells' parameters and their libraries' prior rows (beta_stds constrained,
+  // beta_means), gathered per lane -- any number of libraries
   float u = 0.0f, tau_z = 0.0f, mean_x = 1.0f, ploidy = 1.0f;
   int lib = 0;
-  float bz[K1T];
+  float bz[K1T], lbsd[K1T], lbmn[K1T];
 #pragma unroll
-  for (int k = 0; k < K1T; ++k) bz[k] = 0.0f;
+  for (int k = 0; k < K1T; ++k) { bz[k] = 0.0f; lbsd[k] = 1.0f; lbmn[k] = 0.0f; }
   if (grp == 0 && in_range) {
     u = st.params[lay.off_u + n];
     tau_z = st.params[lay.off_tau + n];
@@ -808,7 +802,11 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
     ploidy = pr.ploidy[n];
 #pragma unroll
     for (int k = 0; k < K1T; ++k)
-      if (k < K1) bz[k] = st.params[lay.off_beta + k * N + n];
+      if (k < K1) {
+        bz[k] = st.params[lay.off_beta + k * N + n];
+        lbsd[k] = st.params[lay.off_bstds + lib * K1 + k];
+        lbmn[k] = step1 ? st.params[lay.off_bmeans + lib * K1 + k] : pr.beta_means[lib * K1 + k];
+      }
   }
   // the enumerated pass's ELBO / d/da sums of this cell tile, one bin tile per thread
   double wl = 0.0, wa = 0.0;
@@ -914,8 +912,8 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
 #pragma unroll
     for (int k = 0; k < K1T; ++k) {
       if (k >= K1) continue;
-      const float bsd = s_bsd[lib * K1 + k];
-      const float bmn = s_bmn[lib * K1 + k];
+      const float bsd = fexp(lbsd[k]);
+      const float bmn = lbmn[k];
       const float b = bz[k];
       const float wk = (b - bmn) / bsd;
       lp += (double)(-0.5f * wk * wk - logf(bsd) - kHalfLog2PiF);
@@ -967,7 +965,7 @@ __device__ void fin_global(const pert_problem& pr, const pert_state& st, int n_b
   const int kind = pr.kind;
   constexpr int kSW = kFinBlock / 64;
   __shared__ double s_red4[kSW][kBlkSlots];
-  __shared__ double s_slot[64];
+  __shared__ double s_tail[2];
   const int lane = tid & 63, wave = tid >> 6;
   // (1) the observed pass's workgroup partials (step 1; none for the enumerated passes):
   //     all 1024 threads, double4 per workgroup, one LDS round
@@ -983,13 +981,30 @@ __device__ void fin_global(const pert_problem& pr, const pert_state& st, int n_b
 #pragma unroll
     for (int j = 0; j < kBlkSlots; ++j) s_red4[wave][j] = v[j];
   }
-  // (2) the cell-block partials: one wave per slot (fixed order)
+  // (2) the cell-block partials: one wave per slot (fixed order), any number of libraries.
+  //     The per-library slots go straight to their gradients; the ELBO and d/da sums to LDS.
   const int nslot = fin_slots(nl, K1);
+  const int nlk = nl * K1;
   for (int sl = wave; sl < nslot; sl += kSW) {
     double acc = 0.0;
     for (int b = lane; b < n_cblk; b += 64) acc += st.cellblk_part[(size_t)b * nslot + sl];
     acc = wave_sum_d(acc);
-    if (lane == 0) s_slot[sl] = acc;
+    if (lane == 0) {
+      if (sl < nlk) {
+        st.grad_shared[lay.off_bstds + sl] = -acc;
+      } else if (sl < 2 * nlk) {
+        const int j = sl - nlk;
+        if (kind == PERT_KIND_STEP1) {
+          const double bm = st.params[lay.off_bmeans + j];
+          // beta_means ~ N(0, 1) (:560): prior gradient -bm added once (root)
+          st.grad_shared[lay.off_bmeans + j] = -(acc + (pr.is_root ? -bm : 0.0));
+        } else {
+          st.grad_shared[lay.off_bmeans + j] = 0.0;
+        }
+      } else {
+        s_tail[sl - 2 * nlk] = acc;
+      }
+    }
   }
   __syncthreads();
   if (tid != 0) return;
@@ -1000,26 +1015,8 @@ __device__ void fin_global(const pert_problem& pr, const pert_state& st, int n_b
     for (int w = 0; w < kSW; ++w) t += s_red4[w][j];
     tot[j] = t;
   }
-  double elbo = tot[0];
-  for (int sl = 0; sl < nslot; ++sl) {
-    const double S = s_slot[sl];
-    if (sl < nl * K1) {
-      st.grad_shared[lay.off_bstds + sl] = -S;
-    } else if (sl < 2 * nl * K1) {
-      const int j = sl - nl * K1;
-      if (kind == PERT_KIND_STEP1) {
-        const double bm = st.params[lay.off_bmeans + j];
-        // beta_means ~ N(0, 1) (:560): prior gradient -bm added once (root)
-        st.grad_shared[lay.off_bmeans + j] = -(S + (pr.is_root ? -bm : 0.0));
-      } else {
-        st.grad_shared[lay.off_bmeans + j] = 0.0;
-      }
-    } else if (sl == 2 * nl * K1) {
-      elbo += S;
-    } else {
-      tot[1] += S;
-    }
-  }
+  double elbo = tot[0] + s_tail[0];
+  tot[1] += s_tail[1];
   // global sites
   if (kind != PERT_KIND_STEP3) {
     const double a = exp((double)st.params[lay.off_a]);
@@ -1260,7 +1257,12 @@ int selftest_enum_host(int64_t n, const float* x, const float* em1, const float*
 // ============================================================================ C ABI
 extern "C" {
 
-const char* pert_version(void) { return "pert_hip 0.1 gfx950"; }
+// "src=<hash>": SHA-256 prefix of the sources this binary was compiled from (build.py
+// source_hash(); _native.lib() refuses a library whose hash differs from its tree)
+#ifndef PERT_SOURCE_HASH
+#define PERT_SOURCE_HASH "unknown"
+#endif
+const char* pert_version(void) { return "pert_hip 0.2 gfx950 src=" PERT_SOURCE_HASH; }
 
 int pert_make_layout(int32_t L, int32_t N, int32_t K1, int32_t n_libs, pert_layout* o) {
   if (!o || L <= 0 || N <= 0 || K1 < 1 || K1 > PERT_MAX_K1 || n_libs < 1) return PERT_E_ARG;
@@ -1372,7 +1374,6 @@ int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream) 
   const int n_lblk = (prob->L + 63) / 64;
   const int n_cblk = (prob->N + 63) / 64;
   const int n_blk = prob->kind == PERT_KIND_STEP1 ? n_bt * n_ct : 0;   // observed pass only
-  if (fin_slots(prob->n_libs, prob->K1) > 64) return PERT_E_ARG;         // fin_global's slot table
   if (prob->K1 == 5)
     hipLaunchKernelGGL(finalize_kernel<5>, dim3(n_cblk + n_lblk), dim3(kFinBlock), 0, stream, *prob, s2, n_cblk,
                        n_bt, n_ct, n_blk);

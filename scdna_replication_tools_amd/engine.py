@@ -296,6 +296,8 @@ class PertShard:
         self.adam_m = torch.zeros(lay.n_params, **f32)
         self.adam_v = torch.zeros(lay.n_params, **f32)
         self.grad_shared = torch.zeros(lay.n_shared + 1, dtype=torch.float64, device=dev)
+        # this shard's own shared-block sums (all-reduced into grad_shared when sharded)
+        self.grad_local = torch.zeros_like(self.grad_shared) if allreduce is not None else self.grad_shared
         self.grad_cell = torch.zeros(lay.n_params - lay.n_shared, **f32)
         self._load_init(init)
 
@@ -468,10 +470,19 @@ class PertShard:
                                                   ctypes.byref(self._hp), mode, s), "pert_enum_pass")
 
     def _finalize(self):
+        """Reductions of the pass partials; with a process group, the shard's shared block is
+        written to ``grad_local`` and the all-reduce runs on a fresh copy of it, so the sum is
+        idempotent: a launch the device loop has already stopped leaves grad_local unchanged
+        and re-reducing it gives the same grad_shared (no world-size blow-up)."""
+        st = self._state
+        if self.allreduce is not None:
+            st.grad_shared = _ptr(self.grad_local)
         with self._dev():
-            nat.check(self.lib.pert_finalize(ctypes.byref(self._prob), ctypes.byref(self._state), self._stream()),
+            nat.check(self.lib.pert_finalize(ctypes.byref(self._prob), ctypes.byref(st), self._stream()),
                       "pert_finalize")
         if self.allreduce is not None:
+            st.grad_shared = _ptr(self.grad_shared)
+            self.grad_shared.copy_(self.grad_local)
             self.allreduce(self.grad_shared)
 
     def step_async(self):

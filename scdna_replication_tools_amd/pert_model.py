@@ -4,20 +4,31 @@ Same constructor arguments and defaults (:37-43), same ``run_pert_model()`` retu
 tuple ``(cn_s_out, supp_s_out_df, cn_g1_out, supp_g1_out_df)`` (:901) and output
 columns (``model_cn_state``, ``model_rep_state``, ``model_tau``, ``model_u``,
 ``model_rho``; supp rows ``model_lambda``, ``model_a``, ``loss_g``, ``loss_s``,
-:466-538).  The three SVI fits run on the GPU through libpert_hip.so
+:466-538), and the reference's public helper methods with their signatures
+(``process_input_data`` :133, ``sort_by_cell_and_loci`` :194, ``get_libraries_tensor``
+:206, ``make_g1_g2_training_data`` :228, ``convert_rt_prior_units`` :254,
+``build_trans_mat`` :260, ``build_cn_prior`` :272, ``build_clone_cn_prior`` :285,
+``build_composite_cn_prior`` :299, ``manhattan_binarization`` :364, ``guess_times`` :426,
+``make_gc_features`` :460, ``package_s_output`` :466).  ``model_s`` (:541, a Pyro model)
+has no counterpart: the SVI fits run on the GPU through libpert_hip.so
 (``engine.PertShard``); there is no CPU path.
 
-Extra keyword arguments (all optional): ``device`` (default ``cuda``),
-``init_method`` ('sampled' = init_to_median(15) draws, 'median' = analytic medians),
-``dirichlet_mode`` ('torch32' reproduces the reference's fp32 Dirichlet normaliser
-in the reported losses, 'exact' = fp64), ``tau_init_method`` ('batched' = all cells'
-GMM / threshold scan at once on the device, tau_init.py; 'sklearn' = the per-cell
-sklearn loop) and ``n_jobs`` for the latter.
+Under ``torch.distributed`` (one process per GPU, world size > 1) every fit is
+cell-sharded over the ranks with one all-reduce of the shared-gradient block per step
+(sharding.py); every rank returns the full outputs.
+
+Extra keyword arguments (all optional): ``device`` (default ``cuda``, or
+``cuda:<LOCAL_RANK>`` under torch.distributed), ``init_method`` ('sampled' =
+init_to_median(15) draws, 'median' = analytic medians), ``dirichlet_mode`` ('torch32'
+reproduces the reference's fp32 Dirichlet normaliser in the reported losses, 'exact' =
+fp64), ``tau_init_method`` ('batched' = all cells' GMM / threshold scan at once on the
+device, tau_init.py; 'sklearn' = the per-cell sklearn loop), ``n_jobs`` for the latter,
+and ``process_group`` (a torch.distributed group; default: the world when initialised).
 """
 from __future__ import annotations
 
 import logging
-import math
+import os
 import time
 from typing import List, Optional
 
@@ -29,6 +40,7 @@ from . import prep
 from ._native import KIND_STEP1, KIND_STEP2, KIND_STEP3
 from .engine import EtaCodebook, PertShard
 from .init import init_params
+from .sharding import cell_bounds, make_allreduce
 from .tau_init import guess_times_batched
 
 log = logging.getLogger("scdna_replication_tools_amd.pert_model")
@@ -42,6 +54,68 @@ def _converged(losses: List[float], i: int, min_iter: int, rel_tol: float) -> bo
     return False
 
 
+def _np(v):
+    if isinstance(v, torch.Tensor):
+        return v.detach().cpu().numpy()
+    return np.asarray(v)
+
+
+class MapTrace:
+    """The part of a Pyro trace that ``package_s_output`` reads (``trace.nodes[name]['value']``),
+    for the MAP values of one fit: expose_u / expose_rho / expose_a / expose_tau and the
+    decoded ``cn`` / ``rep`` (pert_model.py:472-477)."""
+
+    def __init__(self, **values):
+        self.nodes = {k: {"value": v} for k, v in values.items()}
+
+
+class PivotAxes:
+    """``index`` (loci: MultiIndex chr, start) and ``columns`` (cells) of the reference's
+    (loci x cells) read-count frame -- all ``package_s_output`` uses of ``cn_s_reads_df``
+    (:480-499) -- without materialising the frame; ``keys`` carries the sorted long table's
+    integer keys for the fast row lookup."""
+
+    def __init__(self, loci_chr, loci_start, cells, chr_col="chr", start_col="start", cell_col="cell_id",
+                 keys=None):
+        # chr as the category sort_by_cell_and_loci made it (:196-201), as pivot_table keeps it
+        chr_lvl = pd.Categorical(np.asarray(loci_chr).astype(str), categories=prep.CHR_ORDER)
+        self.index = pd.MultiIndex.from_arrays([chr_lvl, np.asarray(loci_start)], names=[chr_col, start_col])
+        self.columns = pd.Index(np.asarray(cells), name=cell_col)
+        self.keys = keys
+
+
+class _Dist:
+    """The process group a fit is sharded over (world 1 = no sharding)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist if dist.is_available() and dist.is_initialized() else None
+        self.group = group
+        self.world = self.dist.get_world_size(group) if self.dist else 1
+        self.rank = self.dist.get_rank(group) if self.dist else 0
+        self.allreduce = make_allreduce(group) if self.world > 1 else None
+        self.backend = self.dist.get_backend(group) if self.dist else None
+
+    def bounds(self, n: int):
+        return cell_bounds(n, self.world)[self.rank]
+
+    def gather_cells(self, a: np.ndarray) -> np.ndarray:
+        """Concatenate the ranks' cell-axis (last axis) blocks of ``a`` in rank order."""
+        if self.world == 1:
+            return a
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
+        t = torch.as_tensor(np.ascontiguousarray(a)).to(dev)
+        n = torch.tensor([t.shape[-1]], device=dev)
+        ns = [torch.zeros_like(n) for _ in range(self.world)]
+        self.dist.all_gather(ns, n, group=self.group)
+        ns = [int(x.item()) for x in ns]
+        pad = torch.zeros(t.shape[:-1] + (max(ns),), dtype=t.dtype, device=dev)
+        pad[..., :t.shape[-1]] = t
+        parts = [torch.empty_like(pad) for _ in range(self.world)]
+        self.dist.all_gather(parts, pad, group=self.group)
+        return torch.cat([p[..., :k] for p, k in zip(parts, ns)], dim=-1).cpu().numpy()
+
+
 class pert_infer_scRT():
     def __init__(self, cn_s, cn_g1, input_col='reads', gc_col='gc', rt_prior_col='mcf7rt',
                  clone_col='clone_id', cell_col='cell_id', library_col='library_id',
@@ -50,7 +124,8 @@ class pert_infer_scRT():
                  cn_prior_weight=1e6, learning_rate=0.05, max_iter=2000, min_iter=100, rel_tol=1e-6,
                  max_iter_step1=None, min_iter_step1=None, max_iter_step3=None, min_iter_step3=None,
                  cuda=False, seed=0, P=13, K=4, J=5, upsilon=6, run_step3=True, *, device=None,
-                 init_method='sampled', dirichlet_mode='torch32', n_jobs=1, tau_init_method='batched'):
+                 init_method='sampled', dirichlet_mode='torch32', n_jobs=1, tau_init_method='batched',
+                 process_group=None):
         self.cn_s = cn_s
         self.cn_g1 = cn_g1
         self.input_col = input_col
@@ -79,31 +154,149 @@ class pert_infer_scRT():
         self.min_iter_step3 = int(self.min_iter / 2) if min_iter_step3 is None else min_iter_step3
         self.cn_prior_method = cn_prior_method
         self.P = P
-        self.L = None
+        self.L = None                         # number of libraries (:214)
         self.K = K
         self.J = J
         self.upsilon = upsilon
         self.run_step3 = run_step3
-        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self._group = process_group
+        if device is None:
+            dist = torch.distributed
+            lr = int(os.environ.get("LOCAL_RANK", "0")) if dist.is_available() and dist.is_initialized() else None
+            device = "cuda" if lr is None else "cuda:{}".format(lr)
+        self.device = torch.device(device)
         self.init_method = init_method
         self.dirichlet_mode = dirichlet_mode
         self.n_jobs = n_jobs
         self.tau_init_method = tau_init_method
         self.timings = {}
         self.iters = {}
+        self._inp = None
 
-    # ------------------------------------------------------------------ prep
+    # ------------------------------------------------------------------ prep (host)
+    def _prepare(self) -> prep.PertInputs:
+        """pert_model.py:133-191, vectorised (prep.process_input_data): sorts and filters
+        self.cn_s / self.cn_g1 like the reference and returns the tensor inputs."""
+        if self._inp is None:
+            self.cn_s, self.cn_g1, inp = prep.process_input_data(
+                self.cn_s, self.cn_g1, input_col=self.input_col, gc_col=self.gc_col, cell_col=self.cell_col,
+                library_col=self.library_col, chr_col=self.chr_col, start_col=self.start_col,
+                cn_state_col=self.cn_state_col)
+            self.L = len(inp.library_ids)
+            self._inp = inp
+        return self._inp
+
+    def _axes(self, cells, keys=None) -> PivotAxes:
+        inp = self._prepare()
+        return PivotAxes(inp.loci_chr, inp.loci_start, cells, self.chr_col, self.start_col, self.cell_col, keys)
+
+    def _frame(self, values, cells) -> pd.DataFrame:
+        ax = self._axes(cells)
+        return pd.DataFrame(values, index=ax.index, columns=ax.columns)
+
     def process_input_data(self):
-        """pert_model.py:133-191 (vectorised, prep.process_input_data)."""
-        self.cn_s, self.cn_g1, inp = prep.process_input_data(
-            self.cn_s, self.cn_g1, input_col=self.input_col, gc_col=self.gc_col, cell_col=self.cell_col,
-            library_col=self.library_col, chr_col=self.chr_col, start_col=self.start_col,
-            cn_state_col=self.cn_state_col)
-        self.L = len(inp.library_ids)
-        return inp
+        """pert_model.py:133-191: returns the reference's 12-tuple (cn_g1_reads_df,
+        cn_g1_states_df, cn_s_reads_df, cn_s_states_df, cn_g1_reads, cn_g1_states, cn_s_reads,
+        cn_s_states, gammas, rt_prior_profile, libs_g1, libs_s).  The (loci x cells) frames
+        hold the int64-truncated values the tensors hold."""
+        inp = self._prepare()
+        t = lambda a: torch.as_tensor(np.asarray(a, np.float32))
+        rt_prior = None
+        if self.rt_prior_col is not None and self.rt_prior_col in self.cn_s.columns:
+            prof = self.cn_s[[self.chr_col, self.start_col, self.rt_prior_col]].drop_duplicates().dropna()
+            rt_prior = self.convert_rt_prior_units(
+                torch.tensor(prof[self.rt_prior_col].values).unsqueeze(-1).to(torch.float32))
+        return (self._frame(inp.reads_g, inp.cells_g), self._frame(inp.states_g, inp.cells_g),
+                self._frame(inp.reads_s, inp.cells_s), self._frame(inp.states_s, inp.cells_s),
+                t(inp.reads_g), t(inp.states_g), t(inp.reads_s), t(inp.states_s), t(inp.gc), rt_prior,
+                torch.as_tensor(inp.libs_g), torch.as_tensor(inp.libs_s))
 
-    def build_etas(self, inp, profiles) -> EtaCodebook:
-        """pert_model.py:668-716."""
+    def sort_by_cell_and_loci(self, cn):
+        """pert_model.py:194-203."""
+        return prep.sort_by_cell_and_loci(cn, self.cell_col, self.chr_col, self.start_col)
+
+    def get_libraries_tensor(self, cn_s, cn_g1):
+        """pert_model.py:206-225: per-cell library index (first-appearance order over S then
+        G1 cells), as int64 tensors; sets self.L to the number of libraries."""
+        libs_s = cn_s[[self.cell_col, self.library_col]].drop_duplicates()
+        libs_g1 = cn_g1[[self.cell_col, self.library_col]].drop_duplicates()
+        ids = pd.concat([libs_s, libs_g1])[self.library_col].unique()
+        self.L = int(len(ids))
+        lut = pd.Series(np.arange(len(ids)), index=ids)
+        return (torch.tensor(libs_s[self.library_col].map(lut).to_numpy()).to(torch.int64),
+                torch.tensor(libs_g1[self.library_col].map(lut).to_numpy()).to(torch.int64))
+
+    def make_g1_g2_training_data(self, cn_g1_states, cn_g1_reads, libs_g1):
+        """pert_model.py:228-251: every G1/2 cell twice, rep = 0 then rep = 1."""
+        libs = torch.cat([libs_g1, libs_g1], dim=0)
+        states = torch.cat([cn_g1_states, cn_g1_states], dim=1)
+        reads = torch.cat([cn_g1_reads, cn_g1_reads], dim=1)
+        rep = torch.cat([torch.zeros(cn_g1_states.shape), torch.ones(cn_g1_states.shape)], dim=1)
+        return states, reads, libs, rep
+
+    def convert_rt_prior_units(self, rt_prior_profile):
+        """pert_model.py:254-257 (the RT prior is parsed but never used by the model)."""
+        return rt_prior_profile / max(rt_prior_profile)
+
+    def build_trans_mat(self, cn):
+        """pert_model.py:260-269 (unused by the reference's fits): eye + 1 plus the counts of
+        state transitions between consecutive loci of every cell."""
+        c = np.asarray(_np(cn)).astype(np.int64)
+        prev, cur = c[:-1].reshape(-1), c[1:].reshape(-1)
+        counts = np.bincount(prev * self.P + cur, minlength=self.P * self.P).reshape(self.P, self.P)
+        return torch.eye(self.P, self.P) + 1 + torch.as_tensor(counts, dtype=torch.float32)
+
+    def build_cn_prior(self, cn, weight=None):
+        """pert_model.py:272-282: dense (loci, cells, P) eta, ones with eta[l, n, cn[l, n]] = weight."""
+        w = self.cn_prior_weight if weight is None else weight
+        return torch.as_tensor(prep.build_cn_prior(_np(cn).astype(np.int64), w, self.P).dense())
+
+    def build_clone_cn_prior(self, cn, cn_df, cn_tensor, clone_cn_profiles):
+        """pert_model.py:285-296: each cell (cn_df.columns) takes its clone's consensus
+        profile (int64-truncated) as prior state; dense (loci, cells, P).  The profile is
+        aligned to cn_df's loci by (chr, start) (the reference indexes it positionally)."""
+        return torch.as_tensor(self._clone_prior(cn, cn_df.columns, clone_cn_profiles, loci=cn_df.index).dense())
+
+    def _clone_prior(self, cn, cells, profiles, loci=None, keys=None) -> EtaCodebook:
+        inp = self._prepare()
+        lc = inp.loci_chr if loci is None else np.asarray(loci.get_level_values(0)).astype(str)
+        ls = inp.loci_start if loci is None else np.asarray(loci.get_level_values(1))
+        return prep.build_clone_cn_prior(cn, np.asarray(cells), lc, ls, profiles, self.cn_prior_weight, self.P,
+                                         self.cell_col, self.clone_col, keys=keys)
+
+    def build_composite_cn_prior(self, cn, clone_cn_profiles, weight=1e5):
+        """pert_model.py:299-361 on the S cells (cn = cn_s_reads_df); dense (loci, cells, P)."""
+        return torch.as_tensor(self._composite_prior(clone_cn_profiles, weight).dense())
+
+    def _composite_prior(self, profiles, weight=1e5) -> EtaCodebook:
+        inp = self._prepare()
+        return prep.build_composite_cn_prior(inp, self.cn_s, self.cn_g1, profiles, self.P, J=self.J, weight=weight,
+                                             cell_col=self.cell_col, clone_col=self.clone_col,
+                                             cn_state_col=self.cn_state_col)
+
+    def manhattan_binarization(self, X, MEAN_GAP_THRESH=0.7, EARLY_S_SKEW_THRESH=0.2, LATE_S_SKEW_THRESH=-0.2):
+        """pert_model.py:364-423 for one cell: (cell_rt, frac_rt)."""
+        return prep.manhattan_binarization(X, MEAN_GAP_THRESH, EARLY_S_SKEW_THRESH, LATE_S_SKEW_THRESH)
+
+    def guess_times(self, cn_s_reads, etas):
+        """pert_model.py:426-457: (t_init, t_alpha_prior, t_beta_prior) as float32 tensors;
+        ``etas`` is the dense (loci, cells, P) prior or an EtaCodebook."""
+        states = etas.argmax_states() if isinstance(etas, EtaCodebook) else torch.argmax(etas, dim=2).numpy()
+        t, a, b = self._guess_times(_np(cn_s_reads), states)
+        return torch.as_tensor(t), torch.as_tensor(a), torch.as_tensor(b)
+
+    def _guess_times(self, reads, cn_states):
+        if self.tau_init_method == 'sklearn':
+            return prep.guess_times(reads, cn_states, self.upsilon, self.n_jobs)
+        return guess_times_batched(reads, cn_states, self.upsilon, device=self.device)
+
+    def make_gc_features(self, x):
+        """pert_model.py:460-463: columns [x^K, ..., x, 1]."""
+        x = x.unsqueeze(1)
+        return torch.cat([x ** i for i in reversed(range(0, self.K + 1))], 1)
+
+    def _build_etas(self, inp, profiles) -> EtaCodebook:
+        """pert_model.py:668-716 as a code book."""
         m, P, w = self.cn_prior_method, self.P, self.cn_prior_weight
         L, N = inp.reads_s.shape
         if m == 'hmmcopy':
@@ -111,21 +304,12 @@ class pert_infer_scRT():
         if m == 'g1_cells':
             return prep.build_g1_cells_prior(inp, self.cn_s, self.cn_g1, w, P, self.cell_col, self.clone_col)
         if m == 'g1_clones':
-            return prep.build_clone_cn_prior(self.cn_s, inp.cells_s, inp.loci_chr, inp.loci_start, profiles, w, P,
-                                             self.cell_col, self.clone_col, keys=inp.keys_s)
+            return self._clone_prior(self.cn_s, inp.cells_s, profiles, keys=inp.keys_s)
         if m == 'g1_composite':
-            return prep.build_composite_cn_prior(inp, self.cn_s, self.cn_g1, profiles, P, J=self.J,
-                                                 cell_col=self.cell_col, clone_col=self.clone_col,
-                                                 cn_state_col=self.cn_state_col)
+            return self._composite_prior(profiles)
         if m == 'diploid':
             return prep.diploid_prior(L, N, w, P)
         return prep.uniform_prior(L, N, P)
-
-    def guess_times(self, reads, cn_states):
-        """pert_model.py:426-457: (t_init, t_alpha_prior, t_beta_prior)."""
-        if self.tau_init_method == 'sklearn':
-            return prep.guess_times(reads, cn_states, self.upsilon, self.n_jobs)
-        return guess_times_batched(reads, cn_states, self.upsilon, device=self.device)
 
     # ------------------------------------------------------------------ fits
     def _svi(self, shard: PertShard, max_iter: int, min_iter: int, label: str) -> List[float]:
@@ -151,23 +335,58 @@ class pert_infer_scRT():
         self.iters[label] = len(losses)
         return losses
 
+    @staticmethod
+    def _cells(init, sl):
+        """The rank's slice of the per-cell entries of an init dict."""
+        out = {}
+        for k, v in init.items():
+            v = np.asarray(v)
+            out[k] = v[sl] if k in ("expose_tau", "expose_u", "expose_betas") else v
+        return out
+
+    def _shard(self, kind, dd: _Dist, reads, libs, init, eta=None, **kw):
+        """PertShard over this rank's contiguous cell range of the fit."""
+        N = reads.shape[1]
+        s0, s1 = dd.bounds(N)
+        sl = slice(s0, s1)
+        if eta is not None:
+            eta = EtaCodebook(np.ascontiguousarray(eta.codes[:, sl]), eta.table)
+        for k in ("cn_obs", "rep_obs"):
+            if k in kw:
+                kw[k] = np.asarray(kw[k])[:, sl]
+        return PertShard(kind, np.ascontiguousarray(reads[:, sl]), self._inp.gc, np.asarray(libs)[sl], self.L,
+                         self.P, self.K, self._cells(init, sl), eta=eta, device=self.device, lr=self.learning_rate,
+                         dirichlet_mode=self.dirichlet_mode, is_root=dd.rank == 0, n_cells_total=N,
+                         allreduce=dd.allreduce, **kw)
+
+    def _decode(self, shard: PertShard, dd: _Dist):
+        cn, rep = shard.decode()
+        c = shard.constrained()
+        cn = dd.gather_cells(cn.cpu().numpy())
+        rep = dd.gather_cells(rep.cpu().numpy())
+        for k in ("expose_tau", "expose_u"):
+            c[k] = dd.gather_cells(np.asarray(c[k]))
+        return cn, rep, c
+
     def run_pert_model(self):
         t_all = time.perf_counter()
         P, K = self.P, self.K
+        dd = _Dist(self._group)
+        if self.device.type == "cuda" and self.device.index is not None:
+            torch.cuda.set_device(self.device)
         tic = time.perf_counter()
-        inp = self.process_input_data()
+        inp = self._prepare()
         n_libs = self.L
         profiles = prep.consensus_clone_profiles(
             self.cn_g1, self.cn_state_col, clone_col=self.clone_col, cell_col=self.cell_col,
             chr_col=self.chr_col, start_col=self.start_col, cn_state_col=self.cn_state_col, keys=inp.keys_g)
-        etas = self.build_etas(inp, profiles)
+        etas = self._build_etas(inp, profiles)
         self.timings["prep"] = time.perf_counter() - tic
 
         # ---- step 1: G1/2 cells doubled, cn / rep observed (:718-774)
         st_g2, rd_g2, lb_g2, rep_g2 = prep.make_g1_g2_training_data(inp.states_g, inp.reads_g, inp.libs_g)
         init1 = init_params(KIND_STEP1, rd_g2, lb_g2, n_libs, P, K, seed=self.seed, method=self.init_method)
-        s1 = PertShard(KIND_STEP1, rd_g2, inp.gc, lb_g2, n_libs, P, K, init1, cn_obs=st_g2, rep_obs=rep_g2,
-                       device=self.device, lr=self.learning_rate, dirichlet_mode=self.dirichlet_mode)
+        s1 = self._shard(KIND_STEP1, dd, rd_g2, lb_g2, init1, cn_obs=st_g2, rep_obs=rep_g2)
         logging.info('STEP 1: Learning reads to CN bias from low variance cells.')
         losses_g = self._svi(s1, self.max_iter_step1, self.min_iter_step1, "step1")
         c1 = s1.constrained()
@@ -177,22 +396,21 @@ class pert_infer_scRT():
 
         # ---- step 2: S cells, enumerated (:776-830)
         tic = time.perf_counter()
-        t_init, _, _ = self.guess_times(inp.reads_s, etas.argmax_states())
+        t_init, _, _ = self._guess_times(inp.reads_s, etas.argmax_states())
         self.timings["guess_times_s"] = time.perf_counter() - tic
         ploidy = etas.argmax_states().astype(np.float32).mean(0)
         init2 = init_params(KIND_STEP2, inp.reads_s, inp.libs_s, n_libs, P, K, ploidy=ploidy, t_init=t_init,
                             beta_means=beta_means_fit, seed=self.seed, method=self.init_method)
-        s2 = PertShard(KIND_STEP2, inp.reads_s, inp.gc, inp.libs_s, n_libs, P, K, init2, eta=etas,
-                       lamb=float(lambda_fit[0]), beta_means=beta_means_fit, device=self.device,
-                       lr=self.learning_rate, dirichlet_mode=self.dirichlet_mode)
+        s2 = self._shard(KIND_STEP2, dd, inp.reads_s, inp.libs_s, init2, eta=etas, lamb=float(lambda_fit[0]),
+                         beta_means=beta_means_fit)
         logging.info('STEP 2: Jointly infer replication and CN states in high variance cells.')
         losses_s = self._svi(s2, self.max_iter, self.min_iter, "step2")
         tic = time.perf_counter()
-        cn_map, rep_map = s2.decode()
-        c2 = s2.constrained()
+        cn_map, rep_map, c2 = self._decode(s2, dd)
+        trace_s = MapTrace(cn=cn_map, rep=rep_map, expose_u=c2["expose_u"], expose_rho=c2["expose_rho"],
+                           expose_a=c2["expose_a"], expose_tau=c2["expose_tau"])
         cn_s_out, supp_s_out_df = self.package_s_output(
-            self.cn_s, inp.cells_s, inp.loci_chr, inp.loci_start, cn_map.cpu().numpy(), rep_map.cpu().numpy(),
-            c2, lambda_fit, losses_g, losses_s, keys=inp.keys_s)
+            self.cn_s, trace_s, self._axes(inp.cells_s, inp.keys_s), lambda_fit, losses_g, losses_s)
         self.timings["decode_package_s"] = time.perf_counter() - tic
         rho_fit = c2["expose_rho"]
         a_fit = c2["expose_a"]
@@ -202,64 +420,73 @@ class pert_infer_scRT():
         if self.run_step3:
             # ---- step 3: G1 cells with rho, a frozen (:834-896)
             tic = time.perf_counter()
-            etas2 = prep.build_clone_cn_prior(self.cn_g1, inp.cells_g, inp.loci_chr, inp.loci_start, profiles,
-                                              self.cn_prior_weight, P, self.cell_col, self.clone_col, keys=inp.keys_g)
-            t_init2, _, _ = self.guess_times(inp.reads_g, etas2.argmax_states())
+            etas2 = self._clone_prior(self.cn_g1, inp.cells_g, profiles, keys=inp.keys_g)
+            t_init2, _, _ = self._guess_times(inp.reads_g, etas2.argmax_states())
             ploidy2 = etas2.argmax_states().astype(np.float32).mean(0)
             self.timings["prep_step3"] = time.perf_counter() - tic
             init3 = init_params(KIND_STEP3, inp.reads_g, inp.libs_g, n_libs, P, K, ploidy=ploidy2,
                                 t_init=t_init2, beta_means=beta_means_fit, seed=self.seed, method=self.init_method)
-            s3 = PertShard(KIND_STEP3, inp.reads_g, inp.gc, inp.libs_g, n_libs, P, K, init3, eta=etas2,
-                           lamb=float(lambda_fit[0]), beta_means=beta_means_fit,
-                           rho_fixed=np.asarray(rho_fit).reshape(-1), a_fixed=float(np.asarray(a_fit)[0]),
-                           device=self.device, lr=self.learning_rate, dirichlet_mode=self.dirichlet_mode)
+            s3 = self._shard(KIND_STEP3, dd, inp.reads_g, inp.libs_g, init3, eta=etas2, lamb=float(lambda_fit[0]),
+                             beta_means=beta_means_fit, rho_fixed=np.asarray(rho_fit).reshape(-1),
+                             a_fixed=float(np.asarray(a_fit)[0]))
             logging.info('STEP 3: Running pre-trained S-phase model on low variance cells.')
             losses_s2 = self._svi(s3, self.max_iter_step3, self.min_iter_step3, "step3")
             tic = time.perf_counter()
-            cn3, rep3 = s3.decode()
-            c3 = s3.constrained()
-            c3["expose_rho"] = rho_fit
-            c3["expose_a"] = a_fit
+            cn3, rep3, c3 = self._decode(s3, dd)
+            trace_s2 = MapTrace(cn=cn3, rep=rep3, expose_u=c3["expose_u"], expose_rho=rho_fit, expose_a=a_fit,
+                                expose_tau=c3["expose_tau"])
             cn_g1_out, supp_g1_out_df = self.package_s_output(
-                self.cn_g1, inp.cells_g, inp.loci_chr, inp.loci_start, cn3.cpu().numpy(), rep3.cpu().numpy(),
-                c3, lambda_fit, losses_g, losses_s2, keys=inp.keys_g)
+                self.cn_g1, trace_s2, self._axes(inp.cells_g, inp.keys_g), lambda_fit, losses_g, losses_s2)
             self.timings["decode_package_g"] = time.perf_counter() - tic
             del s3
         self.timings["total"] = time.perf_counter() - t_all
         return cn_s_out, supp_s_out_df, cn_g1_out, supp_g1_out_df
 
     # ------------------------------------------------------------------ outputs
-    def package_s_output(self, cn, cells, loci_chr, loci_start, model_cn, model_rep, fit, lambda_fit,
-                         losses_g, losses_s, keys=None):
+    def package_s_output(self, cn_s, trace_s, cn_s_reads_df, lambda_fit, losses_g, losses_s):
         """pert_model.py:466-538: per (bin, cell) model_cn_state / model_rep_state, per cell
-        model_tau / model_u, per bin model_rho (inner joins on the long table), plus the
-        supp frame of lambda, a and the loss traces."""
-        if keys is not None and len(keys.cell_code) == len(cn):
+        model_tau / model_u, per bin model_rho -- the rows, row order and dtypes of the
+        reference's melt + inner merges on (cell, chr, start) -- plus the supp frame of
+        lambda, a and the loss traces.  ``trace_s``: a MapTrace (or anything with
+        ``nodes[name]['value']``); ``cn_s_reads_df``: the (loci x cells) frame or a PivotAxes."""
+        nodes = trace_s.nodes
+        v = lambda k: _np(nodes[k]["value"])
+        cells = np.asarray(cn_s_reads_df.columns)
+        idx = cn_s_reads_df.index
+        loci_chr = np.asarray(idx.get_level_values(0)).astype(str)
+        loci_start = np.asarray(idx.get_level_values(1))
+        keys = getattr(cn_s_reads_df, "keys", None)
+        if keys is not None and not isinstance(keys, prep.TableKeys):
+            keys = None                                   # a DataFrame's .keys is a method
+        if keys is not None and len(keys.cell_code) == len(cn_s):
             ci, li = keys.row_positions(cells, loci_chr, loci_start)
         else:
-            cell_index = pd.Index(np.asarray(cells).astype(str))
-            locus_index = pd.MultiIndex.from_arrays([np.asarray(loci_chr).astype(str), np.asarray(loci_start)])
-            ci = cell_index.get_indexer(cn[self.cell_col].astype(str).to_numpy())
+            cell_index = pd.Index(cells.astype(str))
+            locus_index = pd.MultiIndex.from_arrays([loci_chr, loci_start])
+            ci = cell_index.get_indexer(cn_s[self.cell_col].astype(str).to_numpy())
             li = locus_index.get_indexer(pd.MultiIndex.from_arrays(
-                [cn[self.chr_col].astype(str).to_numpy(), cn[self.start_col].to_numpy()]))
+                [cn_s[self.chr_col].astype(str).to_numpy(), cn_s[self.start_col].to_numpy()]))
         keep = (ci >= 0) & (li >= 0)
-        base = cn.loc[keep] if not keep.all() else cn
+        base = cn_s.loc[keep] if not keep.all() else cn_s
         ci, li = ci[keep], li[keep]
+        model_cn, model_rep = v("cn"), v("rep")
         model = pd.DataFrame({
             'model_cn_state': model_cn[li, ci].astype(np.int64),
             'model_rep_state': model_rep[li, ci].astype(np.float32),
-            'model_tau': np.asarray(fit["expose_tau"], dtype=np.float32)[ci],
-            'model_u': np.asarray(fit["expose_u"], dtype=np.float32)[ci],
-            'model_rho': np.asarray(fit["expose_rho"], dtype=np.float32).reshape(-1)[li],
+            'model_tau': v("expose_tau").astype(np.float32).reshape(-1)[ci],
+            'model_u': v("expose_u").astype(np.float32).reshape(-1)[ci],
+            'model_rho': v("expose_rho").astype(np.float32).reshape(-1)[li],
         })
         # new columns side by side with the (sorted) input rows, without copying its blocks
         # (reset_index(drop=True) would deep-copy and consolidate the whole long table)
         base = base.copy(deep=False)
         base.index = pd.RangeIndex(len(base))
         out = pd.concat([base, model], axis=1, copy=False)
+        lam = float(_np(lambda_fit).reshape(-1)[0])
+        a = float(v("expose_a").reshape(-1)[0])
         supp = pd.concat([
-            pd.DataFrame({'param': ['model_lambda'], 'level': ['all'], 'value': [float(lambda_fit[0])]}),
-            pd.DataFrame({'param': ['model_a'], 'level': ['all'], 'value': [float(np.asarray(fit["expose_a"])[0])]}),
+            pd.DataFrame({'param': ['model_lambda'], 'level': ['all'], 'value': [lam]}),
+            pd.DataFrame({'param': ['model_a'], 'level': ['all'], 'value': [a]}),
             pd.DataFrame({'param': ['loss_g'] * len(losses_g), 'level': np.arange(len(losses_g)), 'value': losses_g}),
             pd.DataFrame({'param': ['loss_s'] * len(losses_s), 'level': np.arange(len(losses_s)), 'value': losses_s}),
         ], ignore_index=True)

@@ -193,6 +193,10 @@ class PertInputs:
     library_ids: list
     keys_s: Optional["TableKeys"] = None      # integer keys of the sorted long tables (row order)
     keys_g: Optional["TableKeys"] = None
+    # the input_col pivots before the int64 truncation of :163-166, kept only when the input
+    # is not integer valued: the eta builders correlate the long table's raw values
+    reads_s_raw: Optional[np.ndarray] = None
+    reads_g_raw: Optional[np.ndarray] = None
 
 
 def _trunc32(a):
@@ -260,10 +264,13 @@ def process_input_data(cn_s: pd.DataFrame, cn_g1: pd.DataFrame, input_col="reads
     if np.isnan(gc).any():
         raise ValueError("{} is missing for some loci".format(gc_col))
 
+    reads_s, reads_g = _trunc32(ps_r.values), _trunc32(pg_r.values)
+    raw = lambda v, t: None if np.array_equal(v, t) else v
     inp = PertInputs(loci_chr=ps_r.loci_chr, loci_start=ps_r.loci_start, cells_s=ps_r.cells, cells_g=pg_r.cells,
-                     reads_s=_trunc32(ps_r.values), states_s=_trunc32(ps_s.values),
-                     reads_g=_trunc32(pg_r.values), states_g=_trunc32(pg_s.values), gc=gc,
-                     libs_s=libs_s, libs_g=libs_g, library_ids=all_ids, keys_s=ks, keys_g=kg)
+                     reads_s=reads_s, states_s=_trunc32(ps_s.values),
+                     reads_g=reads_g, states_g=_trunc32(pg_s.values), gc=gc,
+                     libs_s=libs_s, libs_g=libs_g, library_ids=all_ids, keys_s=ks, keys_g=kg,
+                     reads_s_raw=raw(ps_r.values, reads_s), reads_g_raw=raw(pg_r.values, reads_g))
     return cn_s, cn_g1, inp
 
 
@@ -307,11 +314,17 @@ def _majority_ploidy_rows(cn: pd.DataFrame, clone_col="clone_id", cell_col="cell
 
 
 def filter_ploidies(cn: pd.DataFrame, ploidy: Optional[pd.Series] = None, clone_col="clone_id", cell_col="cell_id",
-                    cn_state_col="state"):
-    """filter_ploidies (:17-27): keep the majority ploidy of each clone (ties: smallest)."""
-    if ploidy is None:
+                    cn_state_col="state", ploidy_col: Optional[str] = None):
+    """filter_ploidies (:17-27): keep the rows of the majority ploidy of each clone (row
+    counts, ties to the smallest ploidy; rows of a NaN clone or NaN ploidy dropped).  The
+    per-row ploidy is ``cn[ploidy_col]`` when given, else ``ploidy`` mapped per cell, else
+    each cell's modal state (add_cell_ploidies, :30-39)."""
+    if ploidy_col is not None:
+        pl = cn[ploidy_col].to_numpy()
+    elif ploidy is None:
         return cn[_majority_ploidy_rows(cn, clone_col, cell_col, cn_state_col)]
-    pl = cn[cell_col].map(ploidy).to_numpy()
+    else:
+        pl = cn[cell_col].map(ploidy).to_numpy()
     kc, ku = _factorize(cn[clone_col].to_numpy())
     pc, pu = pd.factorize(pl, sort=True)
     ok = (kc >= 0) & (pc >= 0)
@@ -424,30 +437,122 @@ def pearson_columns(A: np.ndarray, B: np.ndarray) -> np.ndarray:
     return (a.T @ b).cpu().numpy()
 
 
+def compute_cell_corrs(s_cell_cn: pd.DataFrame, clone_cn_g1: pd.DataFrame, s_cell_id, col='rpm_gc_norm',
+                       cell_col='cell_id', chr_col='chr', start_col='start') -> pd.DataFrame:
+    """compute_cell_corrs (normalize_by_cell.py:148-180) for one S cell: Pearson r and its
+    p-value (scipy.stats.pearsonr) between ``col`` of the S cell and of every G1 cell of
+    ``clone_cn_g1`` over the loci both have rows for, G1 cells in ``groupby`` (sorted id)
+    order, then sorted by r descending with pandas' default sort (NaN r last).  The
+    correlation-matched priors use the batched equivalent (``g1_cell_matches``)."""
+    from scipy.stats import pearsonr
+    s_key = pd.MultiIndex.from_arrays([s_cell_cn[chr_col].astype(str).to_numpy(), s_cell_cn[start_col].to_numpy()])
+    s_val = pd.Series(s_cell_cn[col].to_numpy(np.float64), index=s_key)
+    rows = []
+    for g1_cell_id, grp in clone_cn_g1.groupby(cell_col):
+        g_key = pd.MultiIndex.from_arrays([grp[chr_col].astype(str).to_numpy(), grp[start_col].to_numpy()])
+        pos = s_key.get_indexer(g_key)
+        hit = pos >= 0
+        x = s_val.to_numpy()[pos[hit]]
+        y = grp[col].to_numpy(np.float64)[hit]
+        import warnings
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            r, p = pearsonr(x, y)
+        rows.append((s_cell_id, g1_cell_id, float(r), float(p)))
+    out = pd.DataFrame(rows, columns=['s_cell_id', 'g1_cell_id', 'pearson_r', 'pearson_pval'])
+    return out.sort_values(by=['pearson_r'], ascending=False)
+
+
+def rank_desc_like_pandas(vals: np.ndarray) -> np.ndarray:
+    """Row-wise ``DataFrame.sort_values(ascending=False)`` order (default quicksort, NaNs
+    last) as the reference ranks its correlation table (normalize_by_cell.py:177-178):
+    pandas' ``nargsort`` reverses the non-NaN values, argsorts them with numpy's quicksort
+    and reverses the result, so ties come out in the order that procedure gives, which is
+    not the stable one.  NaN-free rows are done as one 2-D argsort; rows holding NaN go
+    through pandas' nargsort itself."""
+    from pandas.core.sorting import nargsort
+    vals = np.asarray(vals, dtype=np.float64)
+    n_rows, n = vals.shape
+    out = np.empty((n_rows, n), dtype=np.int64)
+    nan_rows = np.isnan(vals).any(axis=1)
+    ok = ~nan_rows
+    if ok.any():
+        rev = vals[ok][:, ::-1]
+        o = np.argsort(rev, axis=1, kind="quicksort")
+        out[ok] = (n - 1 - o)[:, ::-1]
+    for r in np.flatnonzero(nan_rows):
+        out[r] = nargsort(vals[r], kind="quicksort", ascending=False, na_position="last")
+    return out
+
+
 def g1_cell_matches(inp: PertInputs, cn_s: pd.DataFrame, cn_g1: pd.DataFrame, J: int, cell_col="cell_id",
                     clone_col: Optional[str] = "clone_id", g1_pool: Optional[pd.DataFrame] = None):
-    """For each S cell, the G1 cells of its clone ranked by Pearson r of the reads over the
-    shared loci, best first (compute_cell_corrs, normalize_by_cell.py:148-180).  Returns an
-    (Ns, J) index array into ``inp.cells_g``."""
+    """For each S cell, its J best-matching G1 cells (pert_model.py:322-345, :677-695):
+    the G1 cells of the S cell's clone in the pool (``cn_g1`` or the majority-ploidy
+    ``g1_pool``), ranked by the Pearson r of ``input_col`` between the two cells
+    (compute_cell_corrs, normalize_by_cell.py:148-180), best first.  Returns an (Ns, J)
+    index array into ``inp.cells_g``.
+
+    The reference correlates each pair over the loci the two cells' rows share (a merge
+    on chr/start of the long tables); its prior assignment then writes the matched G1
+    cell's state rows into the fitted (complete) loci positionally, which only succeeds
+    when that cell's rows are exactly those loci -- so wherever the reference runs, the
+    shared loci are the fitted loci and the pivot's correlations are its correlations.
+    Candidates are ranked in ``groupby(cell_col)`` order (sorted cell ids, the pivot's
+    order) with pandas' sort (``rank_desc_like_pandas``), ties and NaN r included.
+    Raises as the reference does when an S cell's clone has no G1 cell in the pool
+    (ValueError, ``pd.concat`` of nothing) or fewer than J (IndexError, ``iloc[j]``)."""
     pool = cn_g1 if g1_pool is None else g1_pool
     allowed = pd.Index(inp.cells_g).isin(pool[cell_col].unique())
-    corr = pearson_columns(inp.reads_s.astype(np.float64), inp.reads_g.astype(np.float64))
+    rs = inp.reads_s if inp.reads_s_raw is None else inp.reads_s_raw
+    rg = inp.reads_g if inp.reads_g_raw is None else inp.reads_g_raw
+    corr = pearson_columns(np.asarray(rs, np.float64), np.asarray(rg, np.float64))
     if clone_col is not None:
-        cs = first_clone(cn_s, inp.cells_s, cell_col, clone_col)
-        cg = first_clone(pool, inp.cells_g, cell_col, clone_col)
-        same = cs[:, None] == cg[None, :]
+        cs = pd.Series(first_clone(cn_s, inp.cells_s, cell_col, clone_col))
+        cg = pd.Series(first_clone(pool, inp.cells_g, cell_col, clone_col))
+        gkey, guniq = pd.factorize(cg)                              # NaN clone -> -1
+        skey = pd.Index(guniq).get_indexer(cs)                      # S clones unknown to G1 -> -1
+        groups = [(np.flatnonzero(skey == k), np.flatnonzero((gkey == k) & allowed)) for k in range(len(guniq))]
+        missing = np.flatnonzero(skey < 0)
     else:
-        same = np.ones_like(corr, dtype=bool)
-    corr = np.where(same & allowed[None, :], corr, -np.inf)
-    order = np.argsort(-corr, axis=1, kind="stable")[:, :J]
-    return order
+        groups = [(np.arange(corr.shape[0]), np.flatnonzero(allowed))]
+        missing = np.array([], dtype=np.int64)
+    for k, (srows, gcols) in enumerate(groups):
+        if srows.size and gcols.size == 0:
+            missing = np.concatenate([missing, srows])
+    if missing.size:
+        raise ValueError("No objects to concatenate: S cell {} has no G1 cell of its clone to correlate with "
+                         "(compute_cell_corrs)".format(inp.cells_s[int(missing[0])]))
+    out = np.empty((corr.shape[0], J), dtype=np.int64)
+    for srows, gcols in groups:
+        if srows.size == 0:
+            continue
+        if gcols.size < J:
+            raise IndexError("single positional indexer is out-of-bounds: the clone of S cell {} has {} G1 "
+                             "cells in the pool, fewer than J = {}".format(inp.cells_s[int(srows[0])],
+                                                                          gcols.size, J))
+        order = rank_desc_like_pandas(corr[np.ix_(srows, gcols)])[:, :J]
+        out[srows] = gcols[order]
+    return out
 
 
 def build_g1_cells_prior(inp: PertInputs, cn_s, cn_g1, weight: float, P: int, cell_col="cell_id",
                          clone_col="clone_id") -> EtaCodebook:
-    """The ``g1_cells`` branch (pert_model.py:671-701): the best-correlated G1 cell's states."""
+    """The ``g1_cells`` branch (pert_model.py:671-701): the best-correlated G1 cell of the
+    S cell's clone (every G1 cell, no ploidy filter) gives the prior state profile."""
     best = g1_cell_matches(inp, cn_s, cn_g1, 1, cell_col, clone_col)[:, 0]
     return build_cn_prior(inp.states_g[:, best].astype(np.int64), weight, P)
+
+
+def _composite_pool(cn_g1: pd.DataFrame, clone_col: str, cell_col: str, cn_state_col: str,
+                    ploidy_col: str = "ploidy") -> pd.DataFrame:
+    """The G1 rows build_composite_cn_prior draws matches from (pert_model.py:312-317):
+    add_cell_ploidies unless the table already has a ``ploidy`` column, then filter_ploidies
+    (the majority ploidy of each clone, ties to the smallest; rows of a NaN clone dropped)."""
+    if ploidy_col in cn_g1.columns:
+        return filter_ploidies(cn_g1, clone_col=clone_col, cell_col=cell_col, cn_state_col=cn_state_col,
+                               ploidy_col=ploidy_col)
+    return cn_g1[_majority_ploidy_rows(cn_g1, clone_col, cell_col, cn_state_col)]
 
 
 def build_composite_cn_prior(inp: PertInputs, cn_s, cn_g1, profiles: pd.DataFrame, P: int, J: int = 5,
@@ -455,10 +560,14 @@ def build_composite_cn_prior(inp: PertInputs, cn_s, cn_g1, profiles: pd.DataFram
                              cn_state_col="state") -> EtaCodebook:
     """build_composite_cn_prior (pert_model.py:299-361): ones + weight*J*2 at the clone
     consensus state + weight*(J-j) at the j-th best-matching G1 cell's state (G1 cells of
-    the majority ploidy of the clone; J capped by the smallest clone)."""
-    sizes = cn_g1[[cell_col, clone_col]].drop_duplicates().groupby(clone_col).size()
-    J = int(min(J, sizes.min()))
-    pool = cn_g1[_majority_ploidy_rows(cn_g1, clone_col, cell_col, cn_state_col)]
+    the majority ploidy of the clone; J capped by the smallest clone, counted before the
+    ploidy filter as the reference counts it)."""
+    if clone_col is not None:
+        sizes = cn_g1[[cell_col, clone_col]].drop_duplicates().groupby(clone_col).size()
+        J = int(min(J, sizes.min()))
+        pool = _composite_pool(cn_g1, clone_col, cell_col, cn_state_col)
+    else:
+        pool = cn_g1
     match = g1_cell_matches(inp, cn_s, cn_g1, J, cell_col, clone_col, g1_pool=pool)     # (Ns, J)
     clones = first_clone(cn_s, inp.cells_s, cell_col, clone_col)
     clone_state = _profile_matrix(profiles, clones, inp.loci_chr, inp.loci_start).astype(np.int64)

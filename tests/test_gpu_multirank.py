@@ -55,6 +55,9 @@ def _run(kw, z, **extra):
     sh = PertShard(KIND_OF[KIND], init=init, device="cuda:0", **kw, **extra)
     sh.set_unconstrained(z)
     losses, reason = sh.run_svi(ITERS, MIN_ITER, REL_TOL)
+    # the all-reduce is idempotent: launches queued past the device-side stop leave the
+    # reduced loss at the stopping iteration's value (not multiplied by the world size)
+    assert sh.device_loss() == losses[-1], (sh.device_loss(), losses[-1])
     cn, rep = sh.decode()
     return losses, reason, cn.cpu().numpy(), rep.cpu().numpy(), sh.constrained()
 

@@ -126,30 +126,6 @@ def test_clone_prior_matches_dense_reference():
         np.testing.assert_array_equal(dense[:, n], want)
 
 
-def test_package_output_keys_path_matches_lookup_path():
-    from scdna_replication_tools_amd.pert_model import pert_infer_scRT
-    s = _table(8, "s", seed=6)
-    g = _table(6, "g", seed=7)
-    m = pert_infer_scRT(s, g, cn_prior_method='g1_clones', device='cpu')
-    inp = m.process_input_data()
-    L, N = inp.reads_s.shape
-    rng = np.random.default_rng(0)
-    cn = rng.integers(0, 13, (L, N))
-    rep = rng.integers(0, 2, (L, N))
-    fit = {"expose_tau": rng.uniform(size=N), "expose_u": rng.uniform(size=N), "expose_rho": rng.uniform(size=L),
-           "expose_a": np.array([7.0])}
-    args = (m.cn_s, inp.cells_s, inp.loci_chr, inp.loci_start, cn, rep, fit, np.array([0.7]), [1.0], [2.0])
-    a, sa = m.package_s_output(*args, keys=inp.keys_s)
-    b, sb = m.package_s_output(*args)
-    pd.testing.assert_frame_equal(a, b)
-    pd.testing.assert_frame_equal(sa, sb)
-    # spot check: every row carries its own (locus, cell) decode
-    r = a.iloc[5]
-    n = list(inp.cells_s).index(r["cell_id"])
-    l = [i for i in range(L) if inp.loci_chr[i] == str(r["chr"]) and inp.loci_start[i] == r["start"]][0]
-    assert r["model_cn_state"] == cn[l, n] and r["model_rep_state"] == rep[l, n]
-
-
 def test_consensus_matches_reference_golden():
     """prep.consensus_clone_profiles against the reference's own compute_consensus_clone_profiles
     output (tests/golden/make_reference_golden.py; cn_state_col=None path, unsorted rows,

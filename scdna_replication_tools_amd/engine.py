@@ -423,6 +423,27 @@ class PertShard:
         if "expose_pi" in z and self.z_pi is not None:
             self.z_pi.copy_(self.to_tiles(t32(z["expose_pi"])))
 
+    def unconstrained(self, pi_cells=None) -> Dict[str, np.ndarray]:
+        """The unconstrained fp32 storage (oracle site names; inverse of set_unconstrained).
+        ``pi_cells``: include the pi logits of these cells, (L, len, P)."""
+        lay, L, N, K1, nl = self.lay, self.L, self.N, self.K1, self.n_libs
+        p = self.params.cpu().numpy()
+        z = {}
+        if self.kind != nat.KIND_STEP3:
+            z["expose_rho"] = p[lay.off_rho:lay.off_rho + L].reshape(L, 1).copy()
+            z["expose_a"] = p[lay.off_a:lay.off_a + 1].copy()
+        if self.kind == nat.KIND_STEP1:
+            z["expose_lambda"] = p[lay.off_lam:lay.off_lam + 1].copy()
+            z["expose_beta_means"] = p[lay.off_bmeans:lay.off_bmeans + nl * K1].reshape(nl, K1).copy()
+        z["expose_beta_stds"] = p[lay.off_bstds:lay.off_bstds + nl * K1].reshape(nl, K1).copy()
+        z["expose_u"] = p[lay.off_u:lay.off_u + N].copy()
+        z["expose_betas"] = p[lay.off_beta:lay.off_beta + K1 * N].reshape(K1, N).T.copy()
+        z["expose_tau"] = p[lay.off_tau:lay.off_tau + N].copy()
+        if pi_cells is not None and self.z_pi is not None:
+            zp = self.from_tiles(self.z_pi)[:, torch.as_tensor(np.asarray(pi_cells), device=self.device)]
+            z["expose_pi"] = zp.cpu().numpy()
+        return z
+
     def constrained(self) -> Dict[str, np.ndarray]:
         """Current constrained site values (what the reference's trace exposes)."""
         lay, L, N, K1, nl = self.lay, self.L, self.N, self.K1, self.n_libs
@@ -577,8 +598,10 @@ class PertShard:
         self.step_async()
         return self.device_loss()
 
-    def loss_and_grads(self):
-        """-ELBO and d(-ELBO)/dz at the current point, without updating (parity tests)."""
+    def loss_and_grads(self, pi_cells=None):
+        """-ELBO and d(-ELBO)/dz at the current point, without updating (parity tests).
+        ``pi_cells``: return the pi-logit gradient of these cells only (L, len, P) -- the
+        full (L, N, P) array is not copied to the host."""
         if self.kind != nat.KIND_STEP1:
             if self.g_pi is None:
                 self.g_pi = torch.zeros_like(self.z_pi)
@@ -603,7 +626,10 @@ class PertShard:
         g["expose_betas"] = gc[lay.off_beta - off:lay.off_beta - off + K1 * N].reshape(K1, N).T
         g["expose_tau"] = gc[lay.off_tau - off:lay.off_tau - off + N]
         if self.kind != nat.KIND_STEP1:
-            g["expose_pi"] = self.from_tiles(self.g_pi).cpu().numpy()
+            gp = self.from_tiles(self.g_pi)
+            if pi_cells is not None:
+                gp = gp[:, torch.as_tensor(np.asarray(pi_cells), device=gp.device)]
+            g["expose_pi"] = gp.cpu().numpy()
         loss = float(gs[lay.n_shared]) - self.const_total
         if self.pi_block is not None:
             lp, gpi = self.pi_block.logp_and_grad()

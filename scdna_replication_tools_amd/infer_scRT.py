@@ -42,8 +42,11 @@ def assign_s_to_clones(s_phase_cells: pd.DataFrame, clone_df: pd.DataFrame, col_
         x, Y = x[okc], Y[okc]
         xc = x - x.mean()
         Yc = Y - Y.mean(0)
-        r = (xc @ Yc) / (np.linalg.norm(xc) * np.linalg.norm(Yc, axis=0))
-        best.append(clone_df.columns[int(np.nanargmax(r))])
+        with np.errstate(invalid="ignore", divide="ignore"):
+            r = (xc @ Yc) / (np.linalg.norm(xc) * np.linalg.norm(Yc, axis=0))
+        # Series.argmax (:71): first maximum, NaN skipped; all NaN (a constant profile) gives
+        # -1 in the pandas the reference ran on, i.e. the last clone
+        best.append(clone_df.columns[int(np.nanargmax(r)) if np.isfinite(r).any() else -1])
     lut = dict(zip(piv.cells, best))
     s[clone_col] = s[cell_col].astype(str).map(lut)
     return s
@@ -112,6 +115,13 @@ class scRT:
 
     def infer_pert_model(self):
         """infer_scRT.py:127-168."""
+        model = self._pert_model()
+        self.model = model
+        return model.run_pert_model()
+
+    def _pert_model(self) -> pert_infer_scRT:
+        """infer_scRT.py:127-161: clustering (clone_col None), consensus clone profiles of
+        assign_col, S-phase cells assigned to clones, then the PERT model object."""
         if self.clone_col is None:
             # no clone labels: KMeans + BIC over the G1/2 cells' assign_col profiles (:129-138)
             piv = prep.pivot_cells_by_loci(self.cn_g1, self.assign_col, self.cell_col, self.chr_col, self.start_col)
@@ -142,5 +152,4 @@ class scRT:
             min_iter_step1=self.min_iter_step1, min_iter_step3=self.min_iter_step3,
             max_iter_step1=self.max_iter_step1, max_iter_step3=self.max_iter_step3, cuda=self.cuda, seed=self.seed,
             P=self.P, K=self.K, J=self.J, upsilon=self.upsilon, run_step3=self.run_step3, **self.engine_kwargs)
-        self.model = model
-        return model.run_pert_model()
+        return model

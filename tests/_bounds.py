@@ -1,0 +1,126 @@
+"""Elementwise gradient bounds of SURVEY.md Appendix C (test infrastructure).
+
+Every gradient element of the device path must satisfy
+
+    |g_dev - g64| <= RTOL * |g64| + floor
+
+against the fp64 oracle, with RTOL = 1e-4 and the floor
+
+* expose_pi (per bin, cell, state k): 4 eps32 * sum_j (eta_j - 1) * pi_k -- Appendix C's
+  term for the Dirichlet softmax-backward, the cancellation fp32 cannot avoid;
+* every other site: ``FLOOR_C * A`` where A is the sum of the absolute values of the
+  per-(bin, cell) contributions that make up that gradient element (plus its prior
+  term): an fp32 pipeline that evaluates each contribution to a relative accuracy e
+  and sums them cannot be closer than ~e * A to the exact sum where those contributions
+  cancel.  A comes from the oracle itself (``contribution_scale``): the data term is
+  differentiated w.r.t. per-(bin, cell) copies of each site, the absolute values summed
+  over the reduced axis.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from oracle import pert_oracle as po
+
+RTOL = 1e-4
+EPS32 = float(np.finfo(np.float32).eps)
+FLOOR_C = 2e-6          # per-contribution accuracy budget of the fp32 device arithmetic
+
+
+def _expand(z: dict, L: int, N: int) -> dict:
+    """Per-(bin, cell) leaf copies of the sites the data term reads."""
+    ex = {}
+    for name, v in z.items():
+        v = v.detach()
+        if name in ("expose_u", "expose_tau"):
+            ex[name] = v.reshape(1, N).expand(L, N).clone()
+        elif name == "expose_betas":
+            ex[name] = v.reshape(1, N, -1).expand(L, N, v.shape[-1]).clone()
+        elif name == "expose_rho":
+            ex[name] = v.reshape(L, 1).expand(L, N).clone()
+        elif name in ("expose_a", "expose_lambda"):
+            ex[name] = v.reshape(1, 1).expand(L, N).clone()
+        else:
+            ex[name] = v.clone()
+        ex[name].requires_grad_(True)
+    return ex
+
+
+def contribution_scale(prob: po.OracleProblem, z: dict) -> dict:
+    """A per gradient element (see module doc), fp64, shaped like the gradients."""
+    prob = prob.to(torch.float64)
+    z = {k: v.to(torch.float64) for k, v in z.items()}
+    L, N = prob.reads.shape
+    ploidy = po.cell_ploidies(prob)
+    # data term per (bin, cell)
+    ex = _expand(z, L, N)
+    t = po.model_terms(prob, po.constrain(prob.kind, ex), global_terms=False, ploidy=ploidy)
+    data = t["enum"] if "enum" in t else t["reads"] + t["rep"]
+    data.backward()
+    A = {}
+    for name, v in ex.items():
+        if v.grad is None or name == "expose_pi":
+            continue
+        g = v.grad.abs()
+        if name in ("expose_u", "expose_tau"):
+            A[name] = g.sum(0)
+        elif name == "expose_betas":
+            A[name] = g.sum(0)
+        elif name == "expose_rho":
+            A[name] = g.sum(1).reshape(L, 1)
+        elif name in ("expose_a", "expose_lambda"):
+            A[name] = g.sum().reshape(1)
+    # prior terms (one contribution per element, added once)
+    zz = {k: v.detach().clone().requires_grad_(True) for k, v in z.items()}
+    tp = po.model_terms(prob, po.constrain(prob.kind, zz), ploidy=ploidy)
+    prior = sum(v for k, v in tp.items() if k not in ("enum", "reads", "rep", "cn", "expose_pi"))
+    prior.backward()
+    for name, v in zz.items():
+        if name == "expose_pi" or v.grad is None:
+            continue
+        A[name] = A.get(name, torch.zeros_like(v)) + v.grad.abs().reshape(A[name].shape if name in A else v.shape)
+    # beta_stds / beta_means: sums over cells of per-cell prior terms
+    c = po.constrain(prob.kind, {k: v.detach() for k, v in z.items()})
+    bm = c["expose_beta_means"] if prob.kind == "step1" else prob.beta_means.to(torch.float64)
+    bs = c["expose_beta_stds"]
+    w = (c["expose_betas"] - bm[prob.libs]) / bs[prob.libs]
+    per_bs = torch.zeros_like(bs).index_add_(0, prob.libs, (w * w - 1).abs())
+    A["expose_beta_stds"] = per_bs
+    if prob.kind == "step1":
+        A["expose_beta_means"] = torch.zeros_like(bm).index_add_(0, prob.libs, (w / bs[prob.libs]).abs()) + bm.abs()
+    return {k: v.detach().numpy() for k, v in A.items()}
+
+
+def pi_floor(prob: po.OracleProblem, z: dict) -> np.ndarray:
+    """Appendix C: 4 eps32 * sum_j (eta_j - 1) * pi_k per (bin, cell, state)."""
+    pi = torch.softmax(z["expose_pi"].to(torch.float64), -1)
+    S1 = (prob.etas.to(torch.float64) - 1).sum(-1, keepdim=True)
+    return (4 * EPS32 * S1.abs() * pi).numpy()
+
+
+def check(name: str, g_dev, g64, floor) -> float:
+    """Largest |delta| / bound over the tensor (<= 1 passes); raises with the worst element."""
+    g_dev = np.asarray(g_dev, np.float64).reshape(np.shape(g64))
+    g64 = np.asarray(g64, np.float64)
+    bound = RTOL * np.abs(g64) + np.broadcast_to(np.asarray(floor, np.float64), g64.shape)
+    ratio = np.abs(g_dev - g64) / np.maximum(bound, 1e-300)
+    worst = float(ratio.max()) if ratio.size else 0.0
+    if worst > 1.0:
+        i = np.unravel_index(int(ratio.argmax()), ratio.shape)
+        raise AssertionError("{}: |delta| / bound = {:.3g} at {} (dev {:.9g}, fp64 {:.9g}, bound {:.3g})".format(
+            name, worst, i, g_dev[i], g64[i], bound[i]))
+    return worst
+
+
+def check_all(prob: po.OracleProblem, z: dict, g_dev: dict, g64: dict, skip=()) -> dict:
+    """``check`` for every site of g64; returns {site: worst ratio}."""
+    A = contribution_scale(prob, z)
+    out = {}
+    for name, ref in g64.items():
+        if name in skip:
+            continue
+        ref = ref.detach().numpy() if isinstance(ref, torch.Tensor) else np.asarray(ref)
+        floor = pi_floor(prob, z) if name == "expose_pi" else FLOOR_C * A[name].reshape(ref.shape)
+        out[name] = check(name, g_dev[name], ref, floor)
+    return out

@@ -34,9 +34,13 @@ def composite_etas(states_a, states_b, P, rng):
 
 def make_problem(kind: str, L: int = 40, N: int = 70, P: int = 13, K: int = 4, n_libs: int = 2,
                  seed: int = 0, prior: str = "clone", z_scale: float = 1.0, low_reads: bool = False,
-                 reads_fn=None):
+                 reads_fn=None, num_reads=None, subdivide: int = 1):
+    """``L`` bins of the 500 kb grid (or of its ``subdivide``-fold split), ``N`` cells;
+    ``num_reads`` per cell (default: a deep 20x coverage of the 500 kb scDNA regime)."""
     rng = np.random.default_rng(seed)
-    sim = simulate(n_s=N, n_g=N, n_bins=L, seed=seed, num_reads=(2e4 if low_reads else 1e6 * L / 5451 * 20))
+    if num_reads is None:
+        num_reads = 2e4 if low_reads else 1e6 * L / 5451 * 20
+    sim = simulate(n_s=N, n_g=N, n_bins=L, seed=seed, num_reads=num_reads, subdivide=subdivide)
     reads = sim.reads_s.astype(np.float64) if kind != "step1" else sim.reads_g.astype(np.float64)
     if reads_fn is not None:                          # edge cases: all-zero, huge counts
         reads = np.asarray(reads_fn(reads), dtype=np.float64)

@@ -1,0 +1,103 @@
+"""GPU: the three chained fits of run_pert_model (lambda and beta_means
+passed from step 1, beta_stds re-initialised in steps 2/3, rho and a frozen in step 3
+with the clone prior built on the G1/2 cells) against the chained oracle (tests/_chain.py).
+
+* live, on a small two-clone problem under the default g1_composite prior;
+* configs[0]'s stand-in through inference_tutorial.ipynb cell 9's call, verbatim
+  (``from scdna_replication_tools.infer_scRT import scRT; scRT(...).infer(level='pyro')``),
+  against the committed fp32-oracle fixture tests/golden/c1_chain_oracle.npz
+  (tests/golden/make_chain_golden.py): loss traces within 1e-4, decodes >= 99.9 %.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests._chain import oracle_chain, product_arrays
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "c1_chain_oracle.npz")
+
+
+def _compare(prod, ref, loss_rtol=1e-4, min_agree=0.999):
+    report = {}
+    for key in ("losses_g", "losses_s", "losses_s2"):
+        if key not in ref:
+            continue
+        a, b = np.asarray(prod[key]), np.asarray(ref[key])
+        report[key + "_len"] = (len(a), len(b))
+        n = min(len(a), len(b))
+        rel = np.abs(a[:n] - b[:n]) / np.abs(b[:n])
+        report[key + "_maxrel"] = float(rel.max())
+    for cn, rep in (("cn_s", "rep_s"), ("cn_g", "rep_g")):
+        if cn in ref:
+            report[cn + "_agree"] = float(((prod[cn] == ref[cn]) & (prod[rep] == ref[rep])).mean())
+    report["lam_rel"] = float(abs(prod["lam"] - ref["lam"].reshape(-1)[0]) / ref["lam"].reshape(-1)[0])
+    report["a_rel"] = float(abs(prod["a"] - ref["a"].reshape(-1)[0]) / ref["a"].reshape(-1)[0])
+    report["rho_maxabs"] = float(np.abs(prod["rho"] - ref["rho"].reshape(-1)).max())
+    report["tau_s_maxabs"] = float(np.abs(prod["tau_s"] - ref["tau_s"]).max())
+    report["u_s_maxrel"] = float((np.abs(prod["u_s"] - ref["u_s"]) / np.abs(ref["u_s"])).max())
+    print("chain vs oracle:", report)
+    for key in ("losses_g", "losses_s", "losses_s2"):
+        if key in ref:
+            a, b = report[key + "_len"]
+            assert a == b, (key, a, b)                         # same stopping iteration
+            assert report[key + "_maxrel"] <= loss_rtol, (key, report[key + "_maxrel"])
+    for cn in ("cn_s", "cn_g"):
+        if cn in ref:
+            assert report[cn + "_agree"] >= min_agree, (cn, report[cn + "_agree"])
+    assert report["lam_rel"] <= 1e-3 and report["a_rel"] <= 1e-3, report
+    assert report["rho_maxabs"] <= 2e-3 and report["tau_s_maxabs"] <= 2e-3 and report["u_s_maxrel"] <= 1e-3, report
+    return report
+
+
+def test_small_chain_matches_live_oracle_chain():
+    from scdna_replication_tools_amd.pert_model import pert_infer_scRT
+    from scdna_replication_tools_amd.simulator import simulate, to_long_form
+    from scdna_replication_tools_amd.tau_init import guess_times_batched
+    sim = simulate(n_s=36, n_g=36, n_bins=80, num_reads=183 * 80, seed=12, n_clones=2)
+    df_s, df_g = to_long_form(sim, n_libs=2)
+    kw = dict(max_iter=60, min_iter=20, max_iter_step1=40, min_iter_step1=10, max_iter_step3=40, min_iter_step3=10,
+              rel_tol=1e-6, J=3)                           # default cn_prior_method: g1_composite
+    m = pert_infer_scRT(df_s.copy(), df_g.copy(), **kw)
+    out = m.run_pert_model()
+    prod = product_arrays(m, *out)
+    ref_m = pert_infer_scRT(df_s.copy(), df_g.copy(), device="cpu", **kw)
+    ref = oracle_chain(ref_m, torch.float32,
+                       t_init_fn=lambda r, st: guess_times_batched(r, st, 6, device="cuda")[0])
+    _compare(prod, ref)
+
+
+def test_tutorial_cell9_verbatim_matches_chained_oracle_fixture():
+    from tests._configs import C1_COLS_G, C1_COLS_S, c1_tables, input_digest, tutorial_scrt
+    from scdna_replication_tools_amd.tau_init import guess_times_batched
+    fx = dict(np.load(GOLDEN))
+    temp_cn_s, temp_cn_g1, truth = c1_tables()
+    assert input_digest(temp_cn_s, temp_cn_g1) == str(fx["input_digest"]), "stand-in inputs changed"
+
+    # inference_tutorial.ipynb cell 9
+    scrt = tutorial_scrt(temp_cn_s, temp_cn_g1)
+    cn_s_with_scrt, supp_s_output, cn_g_with_scrt, supp_g_output = scrt.infer(level='pyro')
+
+    model_cols = ['model_cn_state', 'model_rep_state', 'model_tau', 'model_u', 'model_rho']
+    assert list(cn_s_with_scrt.columns) == C1_COLS_S + ['clone_id'] + model_cols
+    assert list(cn_g_with_scrt.columns) == C1_COLS_G + model_cols
+    assert len(cn_s_with_scrt) == len(temp_cn_s) and len(cn_g_with_scrt) == len(temp_cn_g1)
+    assert set(supp_s_output.param) == {'model_lambda', 'model_a', 'loss_g', 'loss_s'}
+    assert cn_s_with_scrt['model_cn_state'].dtype == np.int64
+    assert cn_s_with_scrt['model_rep_state'].dtype == np.float32
+
+    inp = scrt.model._prepare()
+    assert list(inp.cells_s) == list(fx["cells_s"]) and list(inp.cells_g) == list(fx["cells_g"])
+    # the product's batched t_init against the per-cell sklearn restatement the fixture used
+    eta_states = np.full(inp.reads_s.shape, 2)
+    t_b = guess_times_batched(inp.reads_s, eta_states, 6, device="cuda")[0]
+    print("t_init: {} of {} cells differ from the sklearn restatement".format(
+        int((t_b != fx["t_init_s"]).sum()), t_b.size))
+    prod = product_arrays(scrt.model, cn_s_with_scrt, supp_s_output, cn_g_with_scrt, supp_g_output)
+    _compare(prod, fx)
+    # and the fit finds the simulated states
+    m = cn_s_with_scrt.merge(truth, on=['cell_id', 'chr', 'start'])
+    assert (m['model_cn_state'] == m['true_somatic_cn']).mean() > 0.99

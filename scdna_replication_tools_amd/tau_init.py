@@ -21,11 +21,19 @@ stage runs as one batched tensor program over the (L, N) matrix with a per-cell
 * skew (scipy ``skew``, biased), linear percentiles, the 100-threshold scan with
   first-minimum ties.
 
-Arithmetic is fp64 (sklearn runs the fit in the profile's fp32), so a cell whose
-scan minimum is a near tie can land one threshold away; tests/test_tau_init.py pins
-the agreement with the per-cell sklearn restatement (``prep.manhattan_binarization``).
+Arithmetic is fp64 while sklearn fits the profile in its own fp32 arithmetic, and read
+counts are integers, so standardised profiles hold many identical values: a group of
+them lying on a k-means decision boundary, an EM lower-bound change at the 1e-3
+tolerance, a mean gap or skew at its threshold, or a near-tie in the threshold scan
+can make the two arithmetics take different branches.  Every such decision is checked
+against a margin (``FRAGILE``, relative) and the cells where any of them falls inside
+it ("fragile" cells, typically under 1 %) are recomputed with the reference's per-cell
+sklearn path (prep.manhattan_binarization), so the result is the reference's for every
+cell; tests/test_tau_init.py pins it.
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import torch
@@ -33,6 +41,23 @@ import torch
 MEAN_GAP_THRESH = 0.7
 EARLY_S_SKEW_THRESH = 0.2
 LATE_S_SKEW_THRESH = -0.2
+# Margins of the decisions fp32 (sklearn) vs fp64 (here) rounding could flip: each is a few
+# times the rounding difference of the quantity compared (validated on simulated profiles:
+# every cell whose batched result differs from the per-cell sklearn one is flagged).  The
+# GMM means sklearn's fp32 EM returns carry ~2e-7 sqrt(L) of rounding (1.5e-6 at 271 bins,
+# 1.4e-5 at 5,451), which moves the scan's levels and thresholds by as much.
+FRAGILE = 1e-5          # relative: mean-gap / skew thresholds
+PP_MARGIN = 2e-6        # relative to the k-means++ potential: candidate draw and choice
+TIE = 1e-6              # relative width of an exact tie on a k-means decision
+EM_MARGIN = 2e-6        # absolute: the EM lower-bound change around its tolerance
+
+
+EPS32 = float(np.finfo(np.float32).eps)
+
+
+def _level_margin(L: int) -> float:
+    """Relative rounding budget of the scan levels b0, b1 (see above)."""
+    return 6e-7 * float(np.sqrt(L))
 
 
 def _rng_draws(n: int):
@@ -45,8 +70,9 @@ def _rng_draws(n: int):
     return first, u
 
 
-def _kmeans_pp(X: torch.Tensor, first: int, u: np.ndarray) -> torch.Tensor:
-    """k-means++ for 2 centres, batched over the columns of X (L, N) -> (2, N)."""
+def _kmeans_pp(X: torch.Tensor, first: int, u: np.ndarray, fragile: torch.Tensor = None) -> torch.Tensor:
+    """k-means++ for 2 centres, batched over the columns of X (L, N) -> (2, N).  Marks in
+    ``fragile`` the columns whose candidate draw or choice is within the rounding margin."""
     L, N = X.shape
     c0 = X[first]                                                    # (N,)
     d0 = (X - c0) ** 2                                               # closest_dist_sq (L, N)
@@ -56,12 +82,34 @@ def _kmeans_pp(X: torch.Tensor, first: int, u: np.ndarray) -> torch.Tensor:
     cand = torch.searchsorted(cums.T.contiguous(), rv.T.contiguous()).clamp_(max=L - 1)  # (N, T)
     xc = torch.gather(X.T, 1, cand)                                  # (N, T) candidate values
     dist_c = torch.minimum(d0[None, :, :], (X[None, :, :] - xc.T[:, None, :]) ** 2)      # (T, L, N)
-    best = dist_c.sum(1).argmin(0)                                   # first minimum (N,)
+    pots = dist_c.sum(1)                                             # (T, N)
+    best = pots.argmin(0)                                            # first minimum (N,)
     c1 = xc.gather(1, best[:, None])[:, 0]
+    if fragile is not None:
+        near = (cums.T.gather(1, cand) - rv.T).abs() <= PP_MARGIN * pot[:, None]
+        prev = cums.T.gather(1, (cand - 1).clamp(min=0))
+        near |= ((prev - rv.T).abs() <= PP_MARGIN * pot[:, None]) & (cand > 0)
+        fragile |= near.any(1)
+        differ = (xc[:, 0] != xc[:, 1]) & ((pots[0] - pots[1]).abs() <= PP_MARGIN * pots.abs().max(0).values)
+        fragile |= differ
     return torch.stack([c0, c1])
 
 
-def _lloyd(X: torch.Tensor, centers: torch.Tensor, tol: torch.Tensor, max_iter: int = 300):
+def _assign(X, c, tie_bias: float = 0.0):
+    """sklearn's label rule: centre 1 where ||c1||^2 - 2 x c1 < ||c0||^2 - 2 x c0.  Points
+    within ``tie_bias`` (relative to the magnitude of the compared values) of the
+    decision go to centre 1 (bias > 0) or centre 0 (bias < 0): with integer read counts
+    whole groups of identical values sit exactly on a decision, where rounding decides."""
+    d1 = c[1] ** 2 - 2 * X * c[1]
+    d0 = c[0] ** 2 - 2 * X * c[0]
+    if tie_bias == 0.0:
+        return (d1 < d0).to(torch.int8)
+    scale = c[0] ** 2 + c[1] ** 2 + 2 * X.abs() * (c[0].abs() + c[1].abs())
+    return (d1 - d0 < tie_bias * scale).to(torch.int8)
+
+
+def _lloyd(X: torch.Tensor, centers: torch.Tensor, tol: torch.Tensor, max_iter: int = 300,
+           fragile: torch.Tensor = None, tie_bias: float = 0.0):
     """Lloyd's k-means for 2 centres, batched; returns the final labels (L, N) bool
     (True = centre 1) after sklearn's stopping rule and final re-assignment."""
     L, N = X.shape
@@ -69,9 +117,11 @@ def _lloyd(X: torch.Tensor, centers: torch.Tensor, tol: torch.Tensor, max_iter: 
     active = torch.ones(N, dtype=torch.bool, device=X.device)
     strict = torch.zeros(N, dtype=torch.bool, device=X.device)
     c = centers.clone()
+    if fragile is None:
+        fragile = torch.zeros(N, dtype=torch.bool, device=X.device)
     for _ in range(max_iter):
-        # pairwise distance as sklearn's chunked kernel ranks it: ||c||^2 - 2 x c, ties to centre 0
-        lab = ((c[1] ** 2 - 2 * X * c[1]) < (c[0] ** 2 - 2 * X * c[0])).to(torch.int8)
+        # pairwise distance as sklearn's chunked kernel ranks it: ||c||^2 - 2 x c
+        lab = _assign(X, c, tie_bias)
         w1 = lab.sum(0).to(X.dtype)
         w0 = L - w1
         s1 = (X * lab).sum(0)
@@ -80,18 +130,19 @@ def _lloyd(X: torch.Tensor, centers: torch.Tensor, tol: torch.Tensor, max_iter: 
                            torch.where(w1 > 0, s1 / w1.clamp(min=1), c[1])])
         shift = ((new - c) ** 2).sum(0)
         same = (lab == labels_old).all(0)
+        fragile |= active & ~same & ((shift - tol).abs() <= FRAGILE * tol)
         c = torch.where(active[None, :], new, c)
         labels_old = torch.where(active[None, :], lab, labels_old)
         strict |= active & same
         active &= ~same & ~(shift <= tol)
         if not bool(active.any()):
             break
-    final = ((c[1] ** 2 - 2 * X * c[1]) < (c[0] ** 2 - 2 * X * c[0])).to(torch.int8)
+    final = _assign(X, c, tie_bias)
     return torch.where(strict[None, :], labels_old, final).bool()
 
 
 def _gmm_means(X: torch.Tensor, lab1: torch.Tensor, max_iter: int = 100, tol: float = 1e-3,
-               reg_covar: float = 1e-6) -> torch.Tensor:
+               reg_covar: float = 1e-6, fragile: torch.Tensor = None) -> torch.Tensor:
     """EM of a 2-component 1-D GaussianMixture from the k-means labels; (2, N) means."""
     L, N = X.shape
     eps10 = 10 * torch.finfo(X.dtype).eps
@@ -121,6 +172,8 @@ def _gmm_means(X: torch.Tensor, lab1: torch.Tensor, max_iter: int = 100, tol: fl
         a = active[None, :]
         w, mu, var = torch.where(a, w2, w), torch.where(a, mu2, mu), torch.where(a, var2, var)
         change = lb2 - lb
+        if fragile is not None:
+            fragile |= active & ((change.abs() - tol).abs() <= EM_MARGIN)
         lb = torch.where(active, lb2, lb)
         active &= ~(change.abs() < tol)
         if not bool(active.any()):
@@ -145,24 +198,39 @@ def _percentiles(X: torch.Tensor, qs) -> torch.Tensor:
     return torch.stack(out)
 
 
-def binarization_fraction(Xraw: torch.Tensor) -> torch.Tensor:
+def binarization_fraction(Xraw: torch.Tensor, return_fragile: bool = False):
     """manhattan_binarization (pert_model.py:364-423) for every column of Xraw (L, N);
-    returns the replicated fraction per column."""
+    returns the replicated fraction per column (and, with ``return_fragile``, the mask of
+    the columns whose outcome fp32 rounding could change, see the module doc): the
+    pipeline runs twice, with ties on a k-means decision broken towards either centre,
+    and a column whose two results differ is fragile too."""
+    if not return_fragile:
+        return _binarize(Xraw, 0.0)[0]
+    f_hi, fr_hi = _binarize(Xraw, TIE)
+    f_lo, fr_lo = _binarize(Xraw, -TIE)
+    return f_hi, fr_hi | fr_lo | (f_hi != f_lo)
+
+
+def _binarize(Xraw: torch.Tensor, tie_bias: float):
     X = Xraw.to(torch.float64)
     L, N = X.shape
     X = (X - X.mean(0)) / X.std(0, unbiased=False)
     first, u = _rng_draws(L)
     Xc = X - X.mean(0)                                               # KMeans centres the data first
     tol = Xc.var(0, unbiased=False) * 1e-4
-    lab1 = _lloyd(Xc, _kmeans_pp(Xc, first, u), tol)
-    mu = _gmm_means(X, lab1)
+    fragile = torch.zeros(N, dtype=torch.bool, device=X.device)
+    lab1 = _lloyd(Xc, _kmeans_pp(Xc, first, u, fragile), tol, fragile=fragile, tie_bias=tie_bias)
+    mu = _gmm_means(X, lab1, fragile=fragile)
     gap = (mu[0] - mu[1]).abs()
     b0, b1 = torch.minimum(mu[0], mu[1]), torch.maximum(mu[0], mu[1])
     close = gap < MEAN_GAP_THRESH
+    fragile |= (gap - MEAN_GAP_THRESH).abs() <= FRAGILE
     if bool(close.any()):
         m2 = (Xc ** 2).mean(0)
         m3 = (Xc ** 3).mean(0)
         skew = m3 / m2 ** 1.5
+        fragile |= close & (((skew - EARLY_S_SKEW_THRESH).abs() <= FRAGILE) |
+                            ((skew - LATE_S_SKEW_THRESH).abs() <= FRAGILE))
         early = close & (skew > EARLY_S_SKEW_THRESH)
         late = close & ~early & (skew < LATE_S_SKEW_THRESH)
         mid = close & ~early & ~late
@@ -181,16 +249,53 @@ def binarization_fraction(Xraw: torch.Tensor) -> torch.Tensor:
         hi = xs[None] > t[:, None, :]                                # (100, L, n)
         d = torch.where(hi, (xs[None] - b1[None, None, s:s + chunk]).abs(),
                         (xs[None] - b0[None, None, s:s + chunk]).abs()).sum(1)     # (100, n)
-        best[s:s + chunk] = t.gather(0, d.argmin(0)[None])[0]        # first minimum
-    return (X > best[None, :]).sum(0).to(torch.float64) / L
+        bi = d.argmin(0)
+        best[s:s + chunk] = t.gather(0, bi[None])[0]                 # first minimum
+        # a near-tie with a threshold that binarises differently, or a point on the threshold
+        # Could the reference pick another threshold?  Its levels differ from these by <= db,
+        # which moves every threshold by <= db and changes d(t) - d(t') only through the points
+        # t and t' binarise differently (<= 2 db each); a point within ~2 db of a threshold may
+        # sit on the other side of it there (changing that d by <= |b1 - b0|); and the
+        # reference sums d in fp32 (pairwise: ~eps32 log2(L) relative).
+        cnt = hi.sum(1)                                              # (100, n)
+        dmin = d.gather(0, bi[None])
+        dcnt = (cnt - cnt.gather(0, bi[None])).abs().to(d.dtype)
+        db = _level_margin(L) * torch.maximum(b0.abs(), b1.abs())[s:s + chunk]
+        span = (b1 - b0)[s:s + chunk].abs()
+        near = ((xs[None] - t[:, None, :]).abs() <= 2 * db[None, None] + 1e-6).sum(1).to(d.dtype)   # (100, n)
+        near_best = near.gather(0, bi[None])
+        slack = (2 * dcnt * db[None] + (near + near_best) * span[None]
+                 + 4 * EPS32 * (np.log2(max(L, 2)) + 2) * dmin)
+        fragile[s:s + chunk] |= (((dcnt > 0) | (near > 0)) & (d - dmin <= slack)).any(0)
+        fragile[s:s + chunk] |= near_best[0] > 0
+    frac = (X > best[None, :]).sum(0).to(torch.float64) / L
+    return frac, fragile
 
 
-def guess_times_batched(reads: np.ndarray, cn_states: np.ndarray, upsilon: float = 6, device=None):
-    """pert_model.py:426-457: (t_init, t_alpha_prior, t_beta_prior), all cells at once."""
+def guess_times_batched(reads: np.ndarray, cn_states: np.ndarray, upsilon: float = 6, device=None,
+                        n_jobs: int = -1):
+    """pert_model.py:426-457: (t_init, t_alpha_prior, t_beta_prior), all cells at once; the
+    fragile cells (module doc) through the reference's per-cell path, on ``n_jobs``
+    processes (-1: the affinity cores, at most 16) when there are many."""
     dev = torch.device(device) if device is not None else torch.device("cpu")
     x = torch.as_tensor(np.asarray(reads, np.float32), device=dev)
     st = torch.as_tensor(np.asarray(cn_states, np.float32), device=dev)
     norm = x / torch.where(st > 0.0, st, torch.full_like(st, 0.5))  # fp32, as the reference divides
-    t = binarization_fraction(norm).to(torch.float32).cpu().numpy()
+    frac, fragile = binarization_fraction(norm, return_fragile=True)
+    t = frac.to(torch.float32).cpu().numpy()
+    redo = np.flatnonzero(fragile.cpu().numpy())
+    if redo.size:
+        from .prep import manhattan_binarization
+        cols = norm[:, torch.as_tensor(redo, device=dev)].cpu().numpy()
+        jobs = [cols[:, j].reshape(-1, 1) for j in range(redo.size)]
+        if redo.size > 64 and n_jobs != 1:
+            from joblib import Parallel, delayed
+            nj = n_jobs if n_jobs > 0 else min(16, len(os.sched_getaffinity(0)))
+            res = Parallel(n_jobs=nj)(delayed(manhattan_binarization)(c) for c in jobs)
+        else:
+            res = [manhattan_binarization(c) for c in jobs]
+        for j, n in enumerate(redo):
+            t[n] = np.float32(res[j][1])
+    guess_times_batched.last_fragile = redo
     alpha = (t * np.float32(upsilon)).astype(np.float32)
     return t, alpha, (np.float32(upsilon) - alpha).astype(np.float32)

@@ -14,7 +14,15 @@ against the fp64 oracle, with RTOL = 1e-4 and the floor
   and sums them cannot be closer than ~e * A to the exact sum where those contributions
   cancel.  A comes from the oracle itself (``contribution_scale``): the data term is
   differentiated w.r.t. per-(bin, cell) copies of each site, the absolute values summed
-  over the reduced axis.
+  over the reduced axis;
+
+plus, for the enumerated fits (steps 2/3), the responsibility term: the joint scores
+s(c, r) are O(x log x) sums an fp32 pipeline holds to ~eps32 * M_s (M_s: the magnitude
+of the terms of that score), and an error ds in the scores moves the contribution
+sum_s gamma_s b_s (b_s = d s_s / d site) by sum_s gamma_s (ds_s - mean ds) (b_s - mean b):
+``SCORE_C * eps32 * sum gamma_s M_s |b_s - b_bar|`` over the reduced axis
+(``score_sensitivity``).  At deep coverage (thousands of reads per bin) this dominates:
+the reference's own fp32 evaluation (lgamma of O(1e4) arguments) is ten times coarser.
 """
 from __future__ import annotations
 
@@ -26,6 +34,7 @@ from oracle import pert_oracle as po
 RTOL = 1e-4
 EPS32 = float(np.finfo(np.float32).eps)
 FLOOR_C = 2e-6          # per-contribution accuracy budget of the fp32 device arithmetic
+SCORE_C = 4.0           # roundings per score term in the device's fp32 score
 
 
 def _expand(z: dict, L: int, N: int) -> dict:
@@ -92,6 +101,63 @@ def contribution_scale(prob: po.OracleProblem, z: dict) -> dict:
     return {k: v.detach().numpy() for k, v in A.items()}
 
 
+def score_magnitudes(prob: po.OracleProblem, z: dict) -> torch.Tensor:
+    """M_s (2P, L, N): the magnitude of the terms the device sums into each joint score --
+    log pi~, log Bern, delta log(1 - lam), and the NB's (delta - 1/2) log1p(x/delta) and
+    x log1p(delta/x) (pert_math.h's asymptotic form)."""
+    with torch.no_grad():
+        c = po.constrain(prob.kind, z)
+        x = prob.reads
+        L, N = x.shape
+        P = prob.P
+        u, betas = c["expose_u"], c["expose_betas"]
+        gcf = po.gc_features(prob.gc, prob.K).reshape(L, 1, -1)
+        omega = torch.exp((betas * gcf).sum(2))
+        lam = prob.lamb
+        cn = torch.arange(P, dtype=x.dtype).reshape(P, 1, 1)
+        rep = torch.tensor([0., 1.], dtype=x.dtype).reshape(2, 1, 1, 1)
+        delta = (u * cn * (1 + rep) * omega * (1 - lam) / lam).clamp(min=1.0)
+        xx = x.expand_as(delta)
+        nb = (delta * torch.log1p(-lam)).abs() + ((delta - 0.5) * torch.log1p(xx / delta)).abs() \
+            + torch.where(xx > 0, xx * torch.log1p(delta / xx.clamp(min=1e-300)), torch.zeros_like(xx)).abs()
+        s = po.enum_scores(prob, z).abs()
+        return (nb + s).reshape(2 * P, L, N)
+
+
+def score_sensitivity(prob: po.OracleProblem, z: dict) -> dict:
+    """SCORE_C eps32 sum gamma_s M_s |b_s - b_bar| per gradient element (module doc)."""
+    prob = prob.to(torch.float64)
+    z = {k: v.to(torch.float64) for k, v in z.items()}
+    L, N = prob.reads.shape
+    P = prob.P
+    ex = _expand(z, L, N)
+    s = po.enum_scores(prob, ex).reshape(2 * P, L, N)
+    gam = torch.softmax(s.detach(), 0)
+    M = score_magnitudes(prob, z)
+    names = [k for k in ex if tuple(ex[k].shape[:2]) == (L, N)]
+    bs = {k: [] for k in names}
+    for i in range(2 * P):
+        gr = torch.autograd.grad(s[i].sum(), [ex[k] for k in names], retain_graph=True, allow_unused=True)
+        for k, g in zip(names, gr):
+            bs[k].append(torch.zeros_like(ex[k]) if g is None else g.detach())
+    out = {}
+    for k in names:
+        b = torch.stack(bs[k])                                    # (2P, L, N[, ...]) per state
+        gm = gam.reshape((2 * P, L, N) + (1,) * (b.dim() - 3))
+        Mm = M.reshape((2 * P, L, N) + (1,) * (b.dim() - 3))
+        bbar = (gm * b).sum(0, keepdim=True)
+        per = SCORE_C * EPS32 * (gm * Mm * (b - bbar).abs()).sum(0)  # per (bin, cell[, ...])
+        if k in ("expose_u", "expose_tau", "expose_betas"):
+            out[k] = per.sum(0)
+        elif k == "expose_rho":
+            out[k] = per.sum(1).reshape(L, 1)
+        elif k in ("expose_a", "expose_lambda"):
+            out[k] = per.sum().reshape(1)
+        elif k == "expose_pi":
+            out[k] = per
+    return {k: v.numpy() for k, v in out.items()}
+
+
 def pi_floor(prob: po.OracleProblem, z: dict) -> np.ndarray:
     """Appendix C: 4 eps32 * sum_j (eta_j - 1) * pi_k per (bin, cell, state)."""
     pi = torch.softmax(z["expose_pi"].to(torch.float64), -1)
@@ -116,11 +182,14 @@ def check(name: str, g_dev, g64, floor) -> float:
 def check_all(prob: po.OracleProblem, z: dict, g_dev: dict, g64: dict, skip=()) -> dict:
     """``check`` for every site of g64; returns {site: worst ratio}."""
     A = contribution_scale(prob, z)
+    S = score_sensitivity(prob, z) if prob.kind != "step1" else {}
     out = {}
     for name, ref in g64.items():
         if name in skip:
             continue
         ref = ref.detach().numpy() if isinstance(ref, torch.Tensor) else np.asarray(ref)
         floor = pi_floor(prob, z) if name == "expose_pi" else FLOOR_C * A[name].reshape(ref.shape)
+        if name in S:
+            floor = floor + S[name].reshape(ref.shape)
         out[name] = check(name, g_dev[name], ref, floor)
     return out

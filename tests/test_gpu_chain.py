@@ -31,6 +31,9 @@ def _compare(prod, ref, loss_rtol=1e-4, min_agree=0.999):
         n = min(len(a), len(b))
         rel = np.abs(a[:n] - b[:n]) / np.abs(b[:n])
         report[key + "_maxrel"] = float(rel.max())
+        i = int(rel.argmax())
+        print(key, "worst at", i, "dev", a[max(0, i - 2):i + 3], "oracle", b[max(0, i - 2):i + 3],
+              "first", a[:3], b[:3])
     for cn, rep in (("cn_s", "rep_s"), ("cn_g", "rep_g")):
         if cn in ref:
             report[cn + "_agree"] = float(((prod[cn] == ref[cn]) & (prod[rep] == ref[rep])).mean())

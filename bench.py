@@ -113,7 +113,7 @@ def main():
     ap.add_argument("--bins-per-tile", type=int, default=0)
     ap.add_argument("--fit", default="step2", choices=["step1", "step2", "step3"],
                     help="which SVI fit's step to time (the metric is step 2's)")
-    ap.add_argument("--variant", type=int, default=0, help="enumerated-pass kernel: 0 LDS-DMA, 1 register")
+    ap.add_argument("--variant", type=int, default=0, help="enumerated-pass kernel: 0 LDS-DMA, 1 register, 3 three-wave streamed")
     ap.add_argument("--cells", type=int, default=0, help="override the config's cell count (per job)")
     ap.add_argument("--subdivide", type=int, default=0, help="override the config's bin subdivision")
     ap.add_argument("--reads-per-cell", type=float, default=1e6, help="synthetic library size per cell")
@@ -241,6 +241,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
                          "kernel": ("obs_kernel" if step1 else
+                                    "enum3_kernel<13, STEP, 5>" if args.variant == 3 else
                                     "enum_dma_kernel<13, STEP, 5>" if args.variant != 1 else "enum_kernel<13, STEP>"),
                          "kernel_ms": kern_ms,
                          "bytes_per_cellbin": bpc,

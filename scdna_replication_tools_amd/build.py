@@ -25,6 +25,7 @@ DEPS = SOURCES + [os.path.join(HERE, "csrc", "pert_math.h"), os.path.join(ROOT, 
 OUT = os.path.join(HERE, "libpert_hip.so")
 ARCH = os.environ.get("PERT_OFFLOAD_ARCH", "gfx950")
 HASH_LEN = 16
+FLAGS = ["-fno-slp-vectorize"]
 
 
 def hipcc() -> str:
@@ -42,6 +43,7 @@ def source_hash() -> str:
         with open(d, "rb") as fh:
             h.update(fh.read())
     h.update(ARCH.encode())
+    h.update(" ".join(FLAGS).encode())
     return h.hexdigest()[:HASH_LEN]
 
 
@@ -61,7 +63,9 @@ def up_to_date() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and up_to_date():
         return OUT
-    cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-shared", "-fPIC",
+    # -fno-slp-vectorize: SLP packs independent fp32 chains into v_pk_* pairs whose register
+    # pairing and shuffles cost 50-70 VGPRs in the enumerated passes (occupancy), for no gain
+    cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-shared", "-fPIC", *FLAGS,
            "-DPERT_SOURCE_HASH=\"{}\"".format(source_hash()),
            "-I" + os.path.join(ROOT, "include"), *SOURCES, "-o", OUT + ".tmp"]
     if verbose:

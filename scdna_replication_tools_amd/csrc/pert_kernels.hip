@@ -565,6 +565,269 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
 }
 
 // ------------------------------------------------------------------------------------------
+// Enumerated pass, three waves per SIMD (variant 3).  One wave per workgroup = 64 cells x LT
+// bins, like enum_dma_kernel, restructured for occupancy: <= 168 VGPRs and <= 13 KB of LDS
+// per wave (12 resident waves per CU instead of 8).
+//  * every streamed array has ONE LDS buffer, refilled by LDS-DMA (buffer_load ... lds, one
+//    voffset VGPR, the bin offset in an SGPR, the pieces as immediate offsets) as soon as the
+//    wave has read it into registers: at the top of bin l, after reading x, the eta code and
+//    the pi logits of bin l, the copies of x, code, logits of bin l+1 and of the Adam moments
+//    of bin l (read in bin l's tail) are issued.  Each buffer is its own __shared__ object,
+//    so the compiler's LDS-DMA tracking waits (counted vmcnt) only for the copy a read needs;
+//  * the per-(bin, cell) arithmetic is enum_online (pert_math.h): the scores are folded into a
+//    running logsumexp group by group, so no per-state array is live; the tail recomputes
+//    pi_k from z and reads the eta row element by element.
+constexpr int kEnum3Group = 6;                  // chi chains interleaved per group
+constexpr int kEnum3TabFloats = 192;            // eta table staged in LDS up to this size
+constexpr unsigned kRsrcWord3 = 0x00020000;     // raw buffer resource, gfx9 data format
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, (int)kRsrcWord3);
+}
+
+// copy a contiguous run of BYTES (multiple of 128) at rsrc + soff into the LDS buffer dst;
+// the run's pieces are immediate offsets from the one SGPR bin offset (the field holds < 4 KB)
+template <int BYTES>
+__device__ __forceinline__ void dma_buf(__amdgpu_buffer_rsrc_t rs, uint32_t soff, float* dst, int lane) {
+  constexpr int n16 = BYTES / 1024;
+  constexpr int rem = BYTES % 1024;
+  static_assert(BYTES % 128 == 0 && BYTES - 128 < 4096, "run longer than the immediate offset field");
+  // the LDS address is cast once from the shared object (folds to a constant M0), the pieces
+  // offset in LDS space -- offsetting the generic pointer would keep a null check per piece
+  typedef __attribute__((address_space(3))) float* lds_f32_t;
+  const lds_f32_t d = (lds_f32_t)dst;
+  pert_static_for<0, n16>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(d + i * 256), 16, lane * 16, soff, i * 1024,
+                                             PERT_DMA_AUX);
+  });
+  pert_static_for<0, rem / 256>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(d + n16 * 256 + i * 64), 4, lane * 4, soff,
+                                             n16 * 1024 + i * 256, PERT_DMA_AUX);
+  });
+  if constexpr (rem % 256 == 128) {
+    if (lane < 32)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(d + (BYTES - 128) / 4), 4, lane * 4, soff,
+                                               BYTES - 128, PERT_DMA_AUX);
+  }
+}
+
+// plane k of a bin: bin and plane offsets in an SGPR (a per-plane voffset would hold a
+// loop-invariant VGPR per plane for the whole pass)
+template <int K>
+__device__ __forceinline__ void store_nt(__amdgpu_buffer_rsrc_t rs, float v, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs, voff, soff + K * 256,
+                                        PERT_NT_STORE ? 2 : 0);
+}
+
+template <int P, int MODE, int K1T>
+__global__ void __launch_bounds__(64, 3) enum3_kernel(pert_problem pr, pert_state st, pert_adam_hparams hp) {
+  constexpr bool kDecode = MODE == PERT_MODE_DECODE;
+  constexpr bool kStep = MODE == PERT_MODE_STEP;
+  constexpr int ZF = P * 64;
+  if (kStep && loop_stopped(st)) return;
+  __shared__ __attribute__((aligned(16))) float s_z[ZF];
+  __shared__ __attribute__((aligned(16))) float s_m[kStep ? ZF : 4];
+  __shared__ __attribute__((aligned(16))) float s_v[kStep ? ZF : 4];
+  __shared__ __attribute__((aligned(16))) float s_xc[96];          // x (64 floats), code (64 x u16)
+  __shared__ float s_bc[kMaxLT * (K1T + 1)];                        // per bin: rho, gcf[K1]
+  __shared__ float s_binp[kDecode ? 1 : kMaxLT];
+  __shared__ float s_tab[kDecode ? 1 : kEnum3TabFloats];
+
+  const int lane = threadIdx.x;
+  const int N = pr.N, K1 = (K1T == PERT_MAX_K1) ? pr.K1 : K1T, ldn = pr.ldn;
+  const int wt = blockIdx.x;
+  const int n = wt * 64 + lane;
+  const bool valid = n < N;
+  const int LT = st.bins_per_tile;
+  const int l0 = blockIdx.y * LT;
+  const int l1 = min(pr.L, l0 + LT);
+  const int nb = l1 - l0;
+  const bool frozen = pr.kind == PERT_KIND_STEP3;
+  const pert_layout lay = st.lay;
+  const float* __restrict__ params = st.params;
+
+  // streamed arrays of this tile as buffer resources (bin offsets < 2^32 within a tile)
+  const size_t tile0 = ((size_t)wt * pr.L + l0) * P * 64;          // floats
+  const uint32_t zbytes = (uint32_t)(nb * P * 256);
+  const __amdgpu_buffer_rsrc_t rz = make_rsrc(st.z_pi + tile0, zbytes);
+  const __amdgpu_buffer_rsrc_t rm = make_rsrc(kStep ? st.m_pi + tile0 : st.z_pi + tile0, zbytes);
+  const __amdgpu_buffer_rsrc_t rv = make_rsrc(kStep ? st.v_pi + tile0 : st.z_pi + tile0, zbytes);
+  const __amdgpu_buffer_rsrc_t rg = make_rsrc(MODE == PERT_MODE_GRAD ? st.g_pi + tile0 : st.z_pi + tile0, zbytes);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(pr.reads + (size_t)l0 * ldn + wt * 64, (uint32_t)(nb * ldn * 4));
+  const __amdgpu_buffer_rsrc_t rc = make_rsrc(pr.eta_code + (size_t)l0 * ldn + wt * 64, (uint32_t)(nb * ldn * 2));
+
+  // first stage in flight before the prologue's parameter loads
+  dma_buf<256>(rx, 0, s_xc, lane);
+  dma_buf<128>(rc, 0, s_xc + 64, lane);
+  dma_buf<P * 256>(rz, 0, s_z, lane);
+
+  // ---- tile prologue: eta table (when small), per-bin rho and GC features, cell parameters
+  const int ntab = pr.n_codes * (P + 1);
+  const bool etal = !kDecode && ntab <= kEnum3TabFloats;
+  if (!kDecode && etal) {
+    for (int i = lane; i < ntab; i += 64) s_tab[i] = pr.eta_table[i];
+  }
+  {
+    const int lr = l0 + min(lane, nb - 1);
+    const float zr = frozen ? pr.rho_fixed[lr] : params[lay.off_rho + lr];
+    const int ng = nb * K1;
+    const float* gsrc = pr.gcf + (size_t)l0 * K1;
+    float gv[PERT_MAX_K1];
+#pragma unroll
+    for (int r = 0; r < PERT_MAX_K1; ++r) gv[r] = gsrc[min(lane + 64 * r, ng - 1)];
+    if (lane < nb) {
+      float dm;
+      s_bc[lane * (K1 + 1)] = frozen ? zr : clipped_sigmoid(zr, &dm);
+    }
+#pragma unroll
+    for (int r = 0; r < PERT_MAX_K1; ++r) {
+      const int i = lane + 64 * r;
+      if (i < ng) {
+        const int lb = i / K1, j = i - lb * K1;
+        s_bc[lb * (K1 + 1) + 1 + j] = gv[r];
+      }
+    }
+  }
+  const float a_val = frozen ? pr.a_fixed : fexp(params[lay.off_a]);
+  const float c0 = (1.0f - pr.lamb) / pr.lamb;
+  const float log1m_lam = pr.log1m_lam;
+  float u = 0.0f, tau = 0.5f;
+  float beta[K1T];
+#pragma unroll
+  for (int k = 0; k < K1T; ++k) beta[k] = 0.0f;
+  if (valid) {
+    u = params[lay.off_u + n];
+#pragma unroll
+    for (int k = 0; k < K1T; ++k)
+      if (k < K1) beta[k] = params[lay.off_beta + k * N + n];
+    float dm;
+    tau = clipped_sigmoid(params[lay.off_tau + n], &dm);
+  }
+  const float ucc = u * c0;
+  float acc[K1T];
+#pragma unroll
+  for (int k = 0; k < K1T; ++k) acc[k] = 0.0f;
+  float sgt = 0.0f, loss = 0.0f, ga = 0.0f;
+  const uint32_t voff = lane * 4;
+
+  __builtin_amdgcn_s_setprio(3);
+  for (int l = l0; l < l1; ++l) {
+    const int lb = l - l0;
+    {
+      const int q4 = 4 * lb;
+      if (q4 >= nb && q4 - 4 < nb) __builtin_amdgcn_s_setprio(2);
+      if (q4 >= 2 * nb && q4 - 4 < 2 * nb) __builtin_amdgcn_s_setprio(1);
+      if (q4 >= 3 * nb && q4 - 4 < 3 * nb) __builtin_amdgcn_s_setprio(0);
+    }
+    // ---- x, eta code and pi logits of bin l into registers; then the copies of bin l+1 and
+    // this bin's Adam moments are issued (they land during the NB chains)
+    const float x = s_xc[lane];
+    const uint32_t code = ((const uint16_t*)(s_xc + 64))[lane];
+    float z[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) z[k] = s_z[k * 64 + lane];
+    const float* bcl = s_bc + lb * (K1 + 1);
+    const float rho = bcl[0];
+    float dot = 0.0f;
+#pragma unroll
+    for (int k = 0; k < K1T; ++k) dot += (k < K1) ? beta[k] * bcl[1 + k] : 0.0f;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // reads done before the buffers refill
+    const uint32_t zoff = (uint32_t)(lb * P * 256);
+    if (l + 1 < l1) {
+      dma_buf<256>(rx, (uint32_t)((lb + 1) * ldn * 4), s_xc, lane);
+      dma_buf<128>(rc, (uint32_t)((lb + 1) * ldn * 2), s_xc + 64, lane);
+      dma_buf<P * 256>(rz, zoff + P * 256, s_z, lane);
+    }
+    if (kStep) {
+      dma_buf<P * 256>(rm, zoff, s_m, lane);
+      dma_buf<P * 256>(rv, zoff, s_v, lane);
+    }
+
+    const float invx = x > 0.0f ? frcp(x) : 0.0f;
+    const float omega = fexp(dot);                         // pert_model.py:633
+    const float D = ucc * omega;                           // :636-640 (delta = chi D)
+    const float t = tau - rho;                             // :616
+    const float phi = frcp(1.0f + fexp(-a_val * t));       // :619
+    EnumOnline<P> o;
+    enum_online<P, kEnum3Group, !kDecode, kDecode>(x, invx, z, log1m_lam, D, phi, o);
+
+    float gtv = 0.0f;
+    if (kDecode) {
+      st.cn_out[(size_t)l * ldn + n] = (uint8_t)(o.argmax % P);
+      st.rep_out[(size_t)l * ldn + n] = (uint8_t)(o.argmax / P);
+    } else {
+      // ---- tail: Dirichlet term, gradient and fused Adam (or the gradient) of the logits, one
+      // plane at a time; the eta row from the LDS copy or from global memory (two copies of
+      // the tail under a wave-uniform branch: one pointer for both would be a flat address)
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+      float dirv = 0.0f;
+      auto tail = [&](const auto* row) {
+        float em[P + 1];                                    // all loads in flight at once
+#pragma unroll
+        for (int k = 0; k <= P; ++k) em[k] = row[k];
+        const float S1 = em[P];
+        pert_static_for<0, P>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          const float em1 = em[k];
+          const float pk = enum_pi(o, z[k], k);
+          dirv += em1 * ((z[k] - o.zmax) - o.lse1p);
+          const float gz = em1 - pk * S1 + o.gcm[k] - pk * o.sgm;
+          const float gl = -gz;                             // d(-ELBO)/dz
+          if (kStep) {
+            const float m1 = hp.beta1 * s_m[k * 64 + lane] + (1.0f - hp.beta1) * gl;
+            const float v1 = hp.beta2 * s_v[k * 64 + lane] + (1.0f - hp.beta2) * gl * gl;
+            const float denom = __builtin_amdgcn_sqrtf(v1) * hp.inv_bc2_sqrt + hp.eps;
+            store_nt<k>(rz, z[k] - hp.step_size * m1 * frcp(denom), voff, zoff);
+            store_nt<k>(rm, m1, voff, zoff);
+            store_nt<k>(rv, v1, voff, zoff);
+          } else {
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, gl), rg, voff, zoff + k * 256, 0);
+          }
+        });
+      };
+      if (etal) tail(s_tab + code * (P + 1));
+      else tail(pr.eta_table + (size_t)code * (P + 1));
+      if (valid) {
+        loss += o.E + dirv;
+        gtv = o.gt;
+        sgt += o.gt;
+        ga += t * o.gt;
+        const float ge = o.gD * omega;
+#pragma unroll
+        for (int k = 0; k < K1T; ++k)
+          if (k < K1) acc[k] += ge * bcl[1 + k];
+      }
+    }
+    if (!kDecode && !frozen) {
+      const float ws = wave_sum(gtv);
+      if (lane == 0) s_binp[lb] = ws;
+    }
+  }
+  if (kDecode) return;
+  if (!frozen) {
+    for (int i = lane; i < nb; i += 64) st.bin_part[(size_t)wt * pr.L + l0 + i] = s_binp[i];
+  }
+  if (valid) {
+    float* cp = st.cell_part + (size_t)blockIdx.y * (K1 + 1) * N + n;
+#pragma unroll
+    for (int k = 0; k < K1T; ++k)
+      if (k < K1) cp[(size_t)k * N] = acc[k];
+    cp[(size_t)K1 * N] = a_val * sgt;
+  }
+  const double bl = wave_sum_d((double)loss);
+  const double bga = wave_sum_d((double)ga);
+  if (lane == 0) {
+    double* bp = st.blk_part + ((size_t)blockIdx.y * (ldn / 64) + wt) * kBlkSlots;
+    bp[0] = bl;
+    bp[1] = bga;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Observed pass (step 1): cn, rep conditioned (pert_model.py:724-729).
 __global__ void __launch_bounds__(kBlock) obs_kernel(pert_problem pr, pert_state st) {
   if (loop_stopped(st)) return;
@@ -1192,10 +1455,15 @@ template <int MODE>
 int launch_enum_mode(int P, dim3 grid, const pert_problem& pr, const pert_state& st,
                      const pert_adam_hparams& hp, hipStream_t s) {
   const bool dma = st.variant != 1;
+  const bool v3 = st.variant == 3;
   switch (P) {
 #define PERT_CASE(PP)                                                                             \
   case PP:                                                                                        \
-    if (dma && pr.K1 == 5)                                                                        \
+    if (v3 && pr.K1 == 5)                                                                         \
+      hipLaunchKernelGGL((enum3_kernel<PP, MODE, 5>), grid, dim3(64), 0, s, pr, st, hp);          \
+    else if (v3)                                                                                  \
+      hipLaunchKernelGGL((enum3_kernel<PP, MODE, PERT_MAX_K1>), grid, dim3(64), 0, s, pr, st, hp); \
+    else if (dma && pr.K1 == 5)                                                                   \
       hipLaunchKernelGGL((enum_dma_kernel<PP, MODE, 5>), grid, dim3(64), dma_lds_bytes(PP, MODE, st, pr), s, pr, st, hp); \
     else if (dma)                                                                                 \
       hipLaunchKernelGGL((enum_dma_kernel<PP, MODE, PERT_MAX_K1>), grid, dim3(64), dma_lds_bytes(PP, MODE, st, pr), s, pr, st, hp); \
@@ -1212,22 +1480,26 @@ int launch_enum_mode(int P, dim3 grid, const pert_problem& pr, const pert_state&
 
 // Resident one-wave workgroups per CU of the STEP-mode LDS-DMA pass at tile length lt.
 template <int P>
-int dma_step_occupancy(const pert_problem& pr, int lt) {
+int dma_step_occupancy(const pert_problem& pr, int lt, int variant) {
   pert_state tmp{};
   tmp.bins_per_tile = lt;
   const size_t lds = dma_lds_bytes(P, PERT_MODE_STEP, tmp, pr);
   int nb = 0;
   hipError_t e;
-  if (pr.K1 == 5)
+  if (variant == 3 && pr.K1 == 5)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, enum3_kernel<P, PERT_MODE_STEP, 5>, 64, 0);
+  else if (variant == 3)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, enum3_kernel<P, PERT_MODE_STEP, PERT_MAX_K1>, 64, 0);
+  else if (pr.K1 == 5)
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, enum_dma_kernel<P, PERT_MODE_STEP, 5>, 64, lds);
   else
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, enum_dma_kernel<P, PERT_MODE_STEP, PERT_MAX_K1>, 64, lds);
   return e == hipSuccess ? nb : 0;
 }
 
-int step_occupancy(const pert_problem& pr, int lt) {
+int step_occupancy(const pert_problem& pr, int lt, int variant) {
   switch (pr.P) {
-#define PERT_CASE(PP) case PP: return dma_step_occupancy<PP>(pr, lt);
+#define PERT_CASE(PP) case PP: return dma_step_occupancy<PP>(pr, lt, variant);
     PERT_CASE(2) PERT_CASE(3) PERT_CASE(4) PERT_CASE(5) PERT_CASE(6) PERT_CASE(7) PERT_CASE(8)
     PERT_CASE(9) PERT_CASE(10) PERT_CASE(11) PERT_CASE(12) PERT_CASE(13) PERT_CASE(14)
     PERT_CASE(15) PERT_CASE(16)
@@ -1319,7 +1591,7 @@ int pert_auto_bins_per_tile(const pert_problem* prob, int32_t variant, int32_t* 
   long best = -1;
   int best_lt = kDefaultLT;
   for (int lt = kMaxLT; lt >= 8; --lt) {
-    const int occ = step_occupancy(*prob, lt);
+    const int occ = step_occupancy(*prob, lt, variant);
     if (occ <= 0) continue;
     const long slots = (long)ncu * occ;
     const long tiles = n_ct * ((prob->L + lt - 1) / lt);

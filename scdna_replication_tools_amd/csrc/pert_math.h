@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #define PERT_HD __host__ __device__ __forceinline__
 
 namespace pert {
@@ -310,6 +312,238 @@ PERT_HD void enum_forward(float x, float invx, const float (&z)[P], float log1m_
   }
   o.gD = gD;
   o.gt = mphi ? (g1 - phic) : 0.0f;
+  o.sgm = sgm;
+}
+
+// ----------------------------------------------------------------- enumerated cell.bin, online form
+// The same per-(bin, cell) arithmetic as enum_forward, arranged for the streamed pass
+// (enum3_kernel) so that no per-state array is ever live: the log pi~ part of every score is
+// formed first (from z), then the chi chains of the NB part run in groups of G and each
+// group's scores are folded into a running logsumexp at once,
+//   M <- max(M, max_group s),  acc <- acc exp(M_old - M) + sum_group exp(s - M),
+// for acc = (sum e, sum e Bc, sum_{r=1} e, e per cn state); the scores and the per-chi delta
+// derivatives Bc = chi (log(1-lam) + Psi) die with their group.  M ends as the exact max of
+// the 2P scores (the logsumexp offset of pert_model.py's enumeration), so E = M + log(sum e)
+// differs from enum_forward by rounding only.  The chains of a group interleave; a
+// scheduling barrier between groups bounds the live temporaries (three waves per SIMD).
+
+template <int I, int N, class F>
+PERT_HD void pert_static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    pert_static_for<I + 1, N>(f);
+  }
+}
+
+template <int P>
+struct ChiList {                 // the chi values the 2P states use, increasing
+  int v[2 * P - 1];
+  int n;
+  constexpr ChiList() : v{}, n(0) {
+    for (int chi = 0; chi < 2 * P - 1; ++chi)
+      if (chi_needed<P>(chi)) v[n++] = chi;
+  }
+  // does a chain among the first `upto` touch cn state c (as (c, 0) or (c, 1))?
+  constexpr bool touches(int upto, int c) const {
+    for (int i = 0; i < upto && i < n; ++i)
+      if (v[i] == c || v[i] == 2 * c) return true;
+    return false;
+  }
+};
+
+template <int P>
+struct EnumOnline {
+  float E;        // logsumexp_{c,r} s(c, r)
+  float gD;       // dE/dD
+  float gt;       // dE/dt / a (masked where phi clamped)
+  float zmax;     // max_k z_k
+  float lse1p;    // log pi_k = z_k - zmax - lse1p
+  float inv1t;    // pi_k = exp(z_k - zmax) inv1t (inv1t for k = jmax)
+  int jmax;       // first argmax of z
+  float sgm;      // sum_k gcm_k
+  float gcm[P];   // gamma^cn_k [pi_k unclamped]
+  int argmax;     // r * P + c of the joint MAP state (first maximum)
+};
+
+// pi_k from the EnumOnline summary, bit-identical to enum_forward's o.pi[k]
+template <int P>
+PERT_HD float enum_pi(const EnumOnline<P>& o, float zk, int k) {
+  return (k == o.jmax) ? o.inv1t : fexp(zk - o.zmax) * o.inv1t;
+}
+
+template <int P, int G, bool WANT_GRAD, bool WANT_ARGMAX>
+PERT_HD void enum_online(float x, float invx, const float (&z)[P], float log1m_lam, float D, float phi_raw,
+                         EnumOnline<P>& o) {
+  // Bernoulli(phi) with the in-place clamps of pert_model.py:622-623
+  float phic = phi_raw;
+  bool mphi = true;
+  if (phic < 0.001f) { phic = 0.001f; mphi = false; }
+  if (phic > 0.999f) { phic = 0.999f; mphi = false; }
+  const float lphi = flog(phic);
+  const float l1mphi = flog(1.0f - phic);
+  // pi = softmax(z), log(clamp_probs(pi)) (transforms.py:951-954, categorical.py:67-71)
+  float m = z[0];
+  int jmax = 0;
+#pragma unroll
+  for (int k = 1; k < P; ++k) { if (z[k] > m) { m = z[k]; jmax = k; } }
+  float lc[P];
+  float t = 0.0f;
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    lc[k] = (k == jmax) ? 1.0f : fexp(z[k] - m);
+    t += (k == jmax) ? 0.0f : lc[k];
+  }
+  const float inv1t = frcp(1.0f + t);
+  const float lse1p = log1p_corr(t, inv1t);
+  uint32_t mk = 0;
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const float pk = lc[k] * inv1t;
+    const float om = (k == jmax) ? t * inv1t : 1.0f - pk;
+    const bool hi = om < kEps32;
+    const bool lo = pk < kEps32;
+    mk |= (hi || lo) ? 0u : (1u << k);
+    lc[k] = hi ? kLog1mEps32 : (lo ? kLogEps32 : (z[k] - m) - lse1p);
+  }
+  o.zmax = m;
+  o.lse1p = lse1p;
+  o.inv1t = inv1t;
+  o.jmax = jmax;
+
+  const float n_clamped = log1m_lam + lambda_delta1(x, invx);   // delta == 1 (chi == 0 or chi D < 1)
+  float M = -INFINITY, se = 0.0f, seB = 0.0f, g1 = 0.0f, best = -INFINITY;
+  int bi = 0;
+  if (WANT_GRAD) {
+#pragma unroll
+    for (int c = 0; c < P; ++c) o.gcm[c] = 0.0f;
+  }
+  constexpr ChiList<P> CL{};
+  constexpr int NG = (CL.n + G - 1) / G;
+
+  auto run = [&](auto asym_c) {
+    constexpr bool ASYM = decltype(asym_c)::value;
+    float rD = 0.0f, ldx = 0.0f;
+    if (ASYM) {
+      rD = frcp(D);
+      ldx = x > 0.0f ? flog(D) - flog(x) : 0.0f;
+    }
+    pert_static_for<0, NG>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+#if defined(__HIP_DEVICE_COMPILE__)
+      if (g > 0) __builtin_amdgcn_sched_barrier(0);
+#endif
+      // the group's NB parts
+      float nn[G], bb[G];
+      pert_static_for<0, G>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        constexpr int idx = g * G + j;
+        if constexpr (idx < CL.n) {
+          constexpr int chi = CL.v[idx];
+          if constexpr (chi == 0) {
+            nn[j] = n_clamped;
+            bb[j] = 0.0f;
+          } else {
+            const float d = (float)chi * D;
+            float lam, psi;
+            if constexpr (ASYM) {
+              nb_lgdiff_asym_hoisted(d, rD * (1.0f / (float)chi), x, ldx + kLogInt[chi], lam, psi);
+              nn[j] = d * log1m_lam + lam;
+              bb[j] = (float)chi * (log1m_lam + psi);
+            } else {
+              if (d < 1.0f) {
+                nn[j] = n_clamped;
+                bb[j] = 0.0f;
+              } else {
+                nb_lgdiff(d, x, invx, lam, psi);
+                nn[j] = d * log1m_lam + lam;
+                bb[j] = (float)chi * (log1m_lam + psi);
+              }
+            }
+          }
+        }
+      });
+      // the group's scores: chain chi feeds (chi, 0) when chi < P and (chi / 2, 1) when even
+      float sg[2 * G];
+      float mg = -INFINITY;
+      pert_static_for<0, G>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        constexpr int idx = g * G + j;
+        if constexpr (idx < CL.n) {
+          constexpr int chi = CL.v[idx];
+          if constexpr (chi < P) {
+            sg[2 * j] = nn[j] + lc[chi] + l1mphi;
+            mg = fmaxf(mg, sg[2 * j]);
+            if (WANT_ARGMAX && (sg[2 * j] > best || (sg[2 * j] == best && chi < bi))) { best = sg[2 * j]; bi = chi; }
+          }
+          if constexpr (chi % 2 == 0) {
+            sg[2 * j + 1] = nn[j] + lc[chi / 2] + lphi;
+            mg = fmaxf(mg, sg[2 * j + 1]);
+            if (WANT_ARGMAX && (sg[2 * j + 1] > best || (sg[2 * j + 1] == best && P + chi / 2 < bi))) {
+              best = sg[2 * j + 1];
+              bi = P + chi / 2;
+            }
+          }
+        }
+      });
+      if (!WANT_GRAD) {
+        M = fmaxf(M, mg);
+        return;
+      }
+      float Mn = mg;
+      if constexpr (g > 0) {
+        Mn = fmaxf(M, mg);
+        const float sc = fexp(M - Mn);
+        se *= sc;
+        seB *= sc;
+        g1 *= sc;
+        pert_static_for<0, P>([&](auto cc) {
+          constexpr int c = decltype(cc)::value;
+          if constexpr (CL.touches(g * G, c)) o.gcm[c] *= sc;
+        });
+      }
+      M = Mn;
+      pert_static_for<0, G>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        constexpr int idx = g * G + j;
+        if constexpr (idx < CL.n) {
+          constexpr int chi = CL.v[idx];
+          float ej = 0.0f;
+          if constexpr (chi < P) {
+            const float e = fexp(sg[2 * j] - M);
+            ej += e;
+            o.gcm[chi] += e;
+          }
+          if constexpr (chi % 2 == 0) {
+            const float e = fexp(sg[2 * j + 1] - M);
+            ej += e;
+            g1 += e;
+            o.gcm[chi / 2] += e;
+          }
+          se += ej;
+          seB += ej * bb[j];
+        }
+      });
+    });
+  };
+  if (D >= kAsymMin) run(std::true_type{});
+  else run(std::false_type{});
+
+  if (WANT_ARGMAX) o.argmax = bi;
+  if (!WANT_GRAD) {
+    o.E = M;
+    return;
+  }
+  const float inv_se = frcp(se);
+  o.E = M + flog(se);
+  o.gD = seB * inv_se;
+  o.gt = mphi ? (g1 * inv_se - phic) : 0.0f;
+  float sgm = 0.0f;
+#pragma unroll
+  for (int c = 0; c < P; ++c) {
+    const float gm = ((mk >> c) & 1u) ? o.gcm[c] * inv_se : 0.0f;
+    o.gcm[c] = gm;
+    sgm += gm;
+  }
   o.sgm = sgm;
 }
 

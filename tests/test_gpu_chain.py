@@ -30,6 +30,12 @@ def _compare(prod, ref, loss_rtol=1e-4, min_agree=0.999):
         report[key + "_len"] = (len(a), len(b))
         n = min(len(a), len(b))
         rel = np.abs(a[:n] - b[:n]) / np.abs(b[:n])
+        if key == "losses_g":
+            # the step-1 ELBO (G1/2 cells, cn and rep observed) crosses zero during the fit,
+            # so the error is taken relative to the trace's scale, max |loss|; the fp32 and
+            # fp64 oracle chains differ by 2e-5 of that scale on the small problem (and by
+            # 4e-4 of the value at the crossing)
+            rel = np.abs(a[:n] - b[:n]) / np.abs(b[:n]).max()
         report[key + "_maxrel"] = float(rel.max())
         i = int(rel.argmax())
         print(key, "worst at", i, "dev", a[max(0, i - 2):i + 3], "oracle", b[max(0, i - 2):i + 3],

@@ -9,7 +9,8 @@
  *   pert_finalize()                  per-cell / per-bin / global gradient reductions
  *   [all-reduce of the shared gradient block across ranks, from the host]
  *   pert_adam()                      Adam on the packed non-pi parameters
- * and the decode is pert_enum_pass(PERT_MODE_DECODE).
+ * and the decode is pert_enum_pass(PERT_MODE_DECODE).  With the three-wave pass (variant 3)
+ * a step of steps 2/3 is instead pert_enum_step() [+ all-reduce + pert_adam_shared()].
  *
  * Conventions: every buffer is device memory owned by the caller (allocated via
  * the torch caching allocator on the caller's side); nothing here allocates.  All
@@ -115,8 +116,9 @@ typedef struct {
   double* blk_part;
   double* cellblk_part;
   int32_t bins_per_tile;           /* LT; 0 = library default */
-  int32_t variant;                 /* enumerated-pass kernel: 0 LDS-DMA streamed (default), 1 register pipelined,
-                                      2 = variant 0 + wave timeline stamps into g_pi (diagnostic, STEP mode) */
+  int32_t variant;                 /* enumerated-pass kernel: 0 LDS-DMA streamed, 1 register pipelined,
+                                      2 = variant 0 + wave timeline stamps into g_pi (diagnostic, STEP mode),
+                                      3 = three waves per SIMD, online logsumexp (pert_enum_step) */
   /* Device-side SVI loop control (the loop of pert_model.py:742-758, :800-816, :867-883).
    * loop_ctl == NULL disables it.  Otherwise pert_adam records the loss of iteration
    * `step` (after the cross-rank all-reduce) into loop_rec and evaluates the reference's
@@ -165,6 +167,24 @@ int pert_auto_bins_per_tile(const pert_problem* prob, int32_t variant, int32_t* 
  * infer_discrete(temperature=0) of :820-827 / :886-893. */
 int pert_enum_pass(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
                    int32_t mode, hipStream_t stream);
+
+/* One whole SVI step of steps 2/3 as ONE launch (variant 3 only): the PERT_MODE_STEP pass
+ * with pert_finalize's reductions folded in -- the last bin tile of each cell tile to finish
+ * reduces that tile's per-cell partials and runs Adam on its cells' u / betas / tau, the last
+ * cell tile of each bin tile reduces that tile's rho partials, and the last of those adds
+ * the global sums into grad_shared (loss in slot n_shared).  update_shared != 0 (a single
+ * rank): the same launch also records the loss for the device loop and runs Adam on the
+ * shared block.  update_shared == 0 (several ranks): all-reduce grad_shared, then
+ * pert_adam_shared().  Uses the arrival counters at the end of cellblk_part (sized by
+ * pert_workspace_sizes, zero-initialised once, re-armed by every launch).
+ * Replaces svi.step() of pert_model.py:801 / :868 with the same update. */
+int pert_enum_step(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
+                   int32_t update_shared, hipStream_t stream);
+
+/* Adam on the shared block [0, n_shared) only (after the all-reduce of a pert_enum_step with
+ * update_shared == 0), plus the device loop's loss record / stopping rule. */
+int pert_adam_shared(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
+                     hipStream_t stream);
 
 /* Observed (step 1) pass: JitTrace_ELBO forward + backward of pert_model.py:743. */
 int pert_obs_pass(const pert_problem* prob, pert_state* st, hipStream_t stream);

@@ -585,31 +585,33 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, (int)kRsrcWord3);
 }
 
-// copy a contiguous run of BYTES (multiple of 128) at rsrc + soff into the LDS buffer dst;
-// the run's pieces are immediate offsets from the one SGPR bin offset (the field holds < 4 KB)
+// copy a contiguous run of BYTES (multiple of 128) at rsrc + soff into the LDS buffer dst.
+// Each piece advances the LDS pointer (M0) and the SGPR offset together and keeps the
+// instruction's immediate offset at 0: the immediate would be added to the LDS address as
+// well as to the global one, and M0 + immediate is not what the pieces want.
 template <int BYTES>
 __device__ __forceinline__ void dma_buf(__amdgpu_buffer_rsrc_t rs, uint32_t soff, float* dst, int lane) {
   constexpr int n16 = BYTES / 1024;
   constexpr int rem = BYTES % 1024;
-  static_assert(BYTES % 128 == 0 && BYTES - 128 < 4096, "run longer than the immediate offset field");
-  // the LDS address is cast once from the shared object (folds to a constant M0), the pieces
-  // offset in LDS space -- offsetting the generic pointer would keep a null check per piece
+  static_assert(BYTES % 128 == 0, "runs are whole half-waves of dwords");
+  // cast once from the shared object (folds to a constant M0 per piece); offsetting the
+  // generic pointer would keep a null check per piece
   typedef __attribute__((address_space(3))) float* lds_f32_t;
   const lds_f32_t d = (lds_f32_t)dst;
   pert_static_for<0, n16>([&](auto ic) {
     constexpr int i = decltype(ic)::value;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(d + i * 256), 16, lane * 16, soff, i * 1024,
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(d + i * 256), 16, lane * 16, soff + i * 1024, 0,
                                              PERT_DMA_AUX);
   });
   pert_static_for<0, rem / 256>([&](auto ic) {
     constexpr int i = decltype(ic)::value;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(d + n16 * 256 + i * 64), 4, lane * 4, soff,
-                                             n16 * 1024 + i * 256, PERT_DMA_AUX);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(d + n16 * 256 + i * 64), 4, lane * 4,
+                                             soff + n16 * 1024 + i * 256, 0, PERT_DMA_AUX);
   });
   if constexpr (rem % 256 == 128) {
     if (lane < 32)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(d + (BYTES - 128) / 4), 4, lane * 4, soff,
-                                               BYTES - 128, PERT_DMA_AUX);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(d + (BYTES - 128) / 4), 4, lane * 4,
+                                               soff + BYTES - 128, 0, PERT_DMA_AUX);
   }
 }
 
@@ -621,8 +623,15 @@ __device__ __forceinline__ void store_nt(__amdgpu_buffer_rsrc_t rs, float v, uin
                                         PERT_NT_STORE ? 2 : 0);
 }
 
+template <int K1T>
+__device__ void enum3_fused_tail(const pert_problem& pr, const pert_state& st, const pert_adam_hparams& hp, int wt,
+                                 int by, int lane, bool update_shared);
+
+// fuse (STEP mode): 0 = partials only (pert_finalize + pert_adam follow), 1 = reductions and the
+// cell sites' Adam folded in (all-reduce + pert_adam_shared follow), 2 = everything folded in
 template <int P, int MODE, int K1T>
-__global__ void __launch_bounds__(64, 3) enum3_kernel(pert_problem pr, pert_state st, pert_adam_hparams hp) {
+__global__ void __launch_bounds__(64, 3) enum3_kernel(pert_problem pr, pert_state st, pert_adam_hparams hp,
+                                                      int fuse) {
   constexpr bool kDecode = MODE == PERT_MODE_DECODE;
   constexpr bool kStep = MODE == PERT_MODE_STEP;
   constexpr int ZF = P * 64;
@@ -825,6 +834,7 @@ __global__ void __launch_bounds__(64, 3) enum3_kernel(pert_problem pr, pert_stat
     bp[0] = bl;
     bp[1] = bga;
   }
+  if (kStep && fuse) enum3_fused_tail<K1T>(pr, st, hp, wt, blockIdx.y, lane, fuse == 2);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1033,6 +1043,69 @@ __device__ __forceinline__ void fin_bins(const pert_problem& pr, const pert_stat
   st.grad_shared[lay.off_rho + l] = (double)a_val * tot * (double)dmask;
 }
 
+// ---- per-cell: the u / beta / tau priors (pert_model.py:585, :597-603) on top of the pass's
+// data sums T[k] (k < K1: sum_l gD omega g_k; k = K1: sum_l a gt) -> the ELBO's derivatives
+// for the cell's sites and its prior log density; dzbs / dbm: the cell's terms of the
+// per-library beta_stds (z = log) and beta_means derivatives.
+template <int K1T>
+struct CellGrads {
+  float dU, dTauZ;
+  float dB[K1T], dzbs[K1T], dbm[K1T];
+  double lp;
+};
+
+template <int K1T, int KCS>
+__device__ __forceinline__ void cell_grads(int K1, bool step1, float c0, float u, float tau_z, float mean_x,
+                                           float ploidy, const float (&bz)[K1T], const float (&lbsd)[K1T],
+                                           const float (&lbmn)[K1T], const double (&T)[KCS], CellGrads<K1T>& o) {
+  double Ak[K1T], Tt = 0.0;
+#pragma unroll
+  for (int k = 0; k < K1T; ++k) Ak[k] = 0.0;
+#pragma unroll
+  for (int k = 0; k < KCS; ++k) {
+    if (k < K1) Ak[k] = T[k];
+    if (k == K1) Tt = T[k];
+  }
+  float dtau_dz;
+  const float tau = clipped_sigmoid(tau_z, &dtau_dz);
+  // data terms: dE/du = c0 sum_l gD omega (intercept column of gcf is 1), dE/dbeta_k = u c0 sum gD omega g_k
+  float dU = c0 * (float)Ak[K1 - 1];
+  float dTau = (float)Tt;
+#pragma unroll
+  for (int k = 0; k < K1T; ++k) o.dB[k] = (k < K1) ? u * c0 * (float)Ak[k] : 0.0f;
+  double lp = 0.0;
+  // u ~ Normal(mu, mu/10), mu = mean(x) / ((1 + tau) ploidy)   (:597-600)
+  const float mu = mean_x / ((1.0f + tau) * ploidy);
+  const float sg = mu / 10.0f;
+  const float w = (u - mu) / sg;
+  lp += (double)(-0.5f * w * w - logf(sg) - kHalfLog2PiF);
+  dU += -w / sg;
+  const float dmu = w / sg + 0.1f * w * w / sg - 0.1f / sg;
+  dTau += dmu * (-mu / (1.0f + tau));
+  // betas ~ Normal(beta_means[lib], beta_stds[lib]).to_event(1)   (:603)
+#pragma unroll
+  for (int k = 0; k < K1T; ++k) {
+    o.dzbs[k] = 0.0f;
+    o.dbm[k] = 0.0f;
+    if (k >= K1) continue;
+    const float bsd = fexp(lbsd[k]);
+    const float wk = (bz[k] - lbmn[k]) / bsd;
+    lp += (double)(-0.5f * wk * wk - logf(bsd) - kHalfLog2PiF);
+    o.dB[k] += -wk / bsd;
+    o.dzbs[k] = wk * wk - 1.0f;          // d/dz_bstds (z = log beta_stds)
+    o.dbm[k] = wk / bsd;                 // d/dbeta_means (step 1)
+  }
+  if (step1) {
+    // tau ~ Beta(1.5, 1.5)  (:585): 0.5 log tau + 0.5 log(1-tau) + lgamma(3) - 2 lgamma(1.5)
+    lp += (double)(0.5f * logf(tau) + 0.5f * logf(1.0f - tau) + 0.69314718055994531f
+                   - 2.0f * (-0.12078223763524522f));
+    dTau += 0.5f / tau - 0.5f / (1.0f - tau);
+  }
+  o.dU = dU;
+  o.dTauZ = dTau * dtau_dz;
+  o.lp = lp;
+}
+
 // ---- per-cell: data sums over bin tiles + u / beta / tau priors -> grad_cell, and the
 // block's per-library beta_stds / beta_means sums, ELBO and d/da into cellblk_part.
 // Everything wave 0 needs besides the sums (its cells' parameters, the per-library prior
@@ -1139,63 +1212,22 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
     float dml;
     lam = 0.001f + 0.998f * clipped_sigmoid(st.params[lay.off_lam], &dml);
   }
-  const float c0 = (1.0f - lam) / lam;
-  double lp = 0.0;
-  float dzbs[K1T], dbm[K1T];
-#pragma unroll
-  for (int k = 0; k < K1T; ++k) { dzbs[k] = 0.0f; dbm[k] = 0.0f; }
+  CellGrads<K1T> cg;
+  cell_grads<K1T>(K1, step1, (1.0f - lam) / lam, u, tau_z, mean_x, ploidy, bz, lbsd, lbmn, T, cg);
   if (valid) {
-    double Ak[K1T], Tt = 0.0;
-#pragma unroll
-    for (int k = 0; k < K1T; ++k) Ak[k] = 0.0;
-#pragma unroll
-    for (int k = 0; k < kCS; ++k) {
-      if (k < K1) Ak[k] = T[k];
-      if (k == K1) Tt = T[k];
-    }
-    float dtau_dz;
-    const float tau = clipped_sigmoid(tau_z, &dtau_dz);
-    // data terms: dE/du = c0 sum_l gD omega (intercept column of gcf is 1), dE/dbeta_k = u c0 sum gD omega g_k
-    float dU = c0 * (float)Ak[K1 - 1];
-    float dTau = (float)Tt;
-    float dB[K1T];
-#pragma unroll
-    for (int k = 0; k < K1T; ++k) dB[k] = (k < K1) ? u * c0 * (float)Ak[k] : 0.0f;
-
-    // u ~ Normal(mu, mu/10), mu = mean(x) / ((1 + tau) ploidy)   (:597-600)
-    const float mu = mean_x / ((1.0f + tau) * ploidy);
-    const float sg = mu / 10.0f;
-    const float w = (u - mu) / sg;
-    lp += (double)(-0.5f * w * w - logf(sg) - kHalfLog2PiF);
-    dU += -w / sg;
-    const float dmu = w / sg + 0.1f * w * w / sg - 0.1f / sg;
-    dTau += dmu * (-mu / (1.0f + tau));
-
-    // betas ~ Normal(beta_means[lib], beta_stds[lib]).to_event(1)   (:603)
-#pragma unroll
-    for (int k = 0; k < K1T; ++k) {
-      if (k >= K1) continue;
-      const float bsd = fexp(lbsd[k]);
-      const float bmn = lbmn[k];
-      const float b = bz[k];
-      const float wk = (b - bmn) / bsd;
-      lp += (double)(-0.5f * wk * wk - logf(bsd) - kHalfLog2PiF);
-      dB[k] += -wk / bsd;
-      dzbs[k] = wk * wk - 1.0f;          // d/dz_bstds (z = log beta_stds)
-      dbm[k] = wk / bsd;                 // d/dbeta_means (step 1)
-    }
-    if (step1) {
-      // tau ~ Beta(1.5, 1.5)  (:585): 0.5 log tau + 0.5 log(1-tau) + lgamma(3) - 2 lgamma(1.5)
-      lp += (double)(0.5f * logf(tau) + 0.5f * logf(1.0f - tau) + 0.69314718055994531f
-                     - 2.0f * (-0.12078223763524522f));
-      dTau += 0.5f / tau - 0.5f / (1.0f - tau);
-    }
     float* gc = st.grad_cell - lay.n_shared;
-    gc[lay.off_u + n] = -dU;
+    gc[lay.off_u + n] = -cg.dU;
 #pragma unroll
     for (int k = 0; k < K1T; ++k)
-      if (k < K1) gc[lay.off_beta + k * N + n] = -dB[k];
-    gc[lay.off_tau + n] = -dTau * dtau_dz;
+      if (k < K1) gc[lay.off_beta + k * N + n] = -cg.dB[k];
+    gc[lay.off_tau + n] = -cg.dTauZ;
+  }
+  const double lp = valid ? cg.lp : 0.0;
+  float dzbs[K1T], dbm[K1T];
+#pragma unroll
+  for (int k = 0; k < K1T; ++k) {
+    dzbs[k] = cg.dzbs[k];
+    dbm[k] = cg.dbm[k];
   }
   // per-library sums for beta_stds (and beta_means in step 1), the ELBO and d/da:
   // wave 0 holds every value, one wave reduction per slot, fixed order
@@ -1386,14 +1418,349 @@ __device__ void loop_record(const pert_state& st) {
   }
 }
 
+// Adam of one packed parameter (torch.optim.Adam; the adam_kernel arithmetic)
+__device__ __forceinline__ void adam_one(const pert_state& st, const pert_adam_hparams& hp, int i, float g) {
+  float mm = st.adam_m[i], vv = st.adam_v[i];
+  mm = hp.beta1 * mm + (1.0f - hp.beta1) * g;
+  vv = hp.beta2 * vv + (1.0f - hp.beta2) * g * g;
+  const float denom = sqrtf(vv) * hp.inv_bc2_sqrt + hp.eps;
+  st.params[i] -= hp.step_size * mm / denom;
+  st.adam_m[i] = mm;
+  st.adam_v[i] = vv;
+}
+
+// ------------------------------------------------------------------------------------------
+// The reductions of an enumerated STEP pass folded into the pass itself (pert_enum_step):
+// every workgroup (64 cells x LT bins, one wave) publishes its partials and counts itself in;
+//  * per cell tile, bin tiles are counted in groups of ~sqrt(n_bt): the last of a group sums the
+//    group's per-cell partials into a level-1 row, and the last level-1 row of the cell tile
+//    sums those, applies the u / beta / tau priors and runs Adam on the tile's cell sites at
+//    once (nothing reads them again in this launch) -- the finalize + adam of the unfused
+//    sequence for that tile, overlapped with the rest of the pass;
+//  * per bin tile, the last cell tile to arrive sums the tile's rho partials over the cell
+//    tiles (and with update_shared, runs Adam on those rho);
+//  * the last of those finalizers adds the global sums (beta_stds, a, the loss) and, with
+//    update_shared (a single rank: no all-reduce between the sums and Adam), records the
+//    loss for the device loop and runs Adam on a and beta_stds.
+// Sums are in fixed order (level 0 in bin-tile order within the group, level 1 in group
+// order, cell tiles in order), so the result does not depend on arrival order.  Publishing
+// is the agent-scope release/acquire pattern of finalize_kernel (__threadfence around the
+// counter atomics); every counter is re-armed by the workgroup that consumed it.
+// bin tiles per level-0 group: about sqrt(n_bt), so both levels stay short (C4: 13 x 14,
+// C5 at LT 32: 66 x 65)
+__device__ __forceinline__ int fused_g1(int n_bt) {
+  int g = 8;
+  while (g * g < n_bt) ++g;
+  return g;
+}
+__device__ __forceinline__ int fused_n_g1(int n_bt) { const int g = fused_g1(n_bt); return (n_bt + g - 1) / g; }
+
+// s[k] += sum_{j < n} p[j rs + k ps] for k < np, in j order; 8 rows x NP planes of loads in
+// flight per round trip (clamped indices, masked values: no guarded loads)
+template <int NP>
+__device__ __forceinline__ void sum_rows(const float* __restrict__ p, size_t rs, size_t ps, int np, int n,
+                                         double (&s)[NP]) {
+  constexpr int R = NP >= 6 ? 4 : 8;                        // rows per round trip
+  for (int j0 = 0; j0 < n; j0 += R) {
+    float v[R][NP];
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        const int j = j0 + u;
+        const float x = p[(size_t)min(j, n - 1) * rs + (size_t)min(k, np - 1) * ps];
+        v[u][k] = (j < n && k < np) ? x : 0.0f;
+      }
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+#pragma unroll
+      for (int k = 0; k < NP; ++k) s[k] += (double)v[u][k];
+  }
+}
+
+// counters after finalize's arrival counter in cellblk_part: [n_ct][n_g1] group, [n_ct]
+// level-1, [n_bt] bin, [1] global
+__device__ __forceinline__ unsigned int* fused_counters(const pert_problem& pr, const pert_state& st) {
+  const int n_cblk = (pr.N + 63) / 64;
+  return reinterpret_cast<unsigned int*>(st.cellblk_part + (size_t)n_cblk * fin_slots(pr.n_libs, pr.K1) + 1);
+}
+
+__device__ __forceinline__ bool wave_flag(bool v) {
+  return __builtin_amdgcn_readfirstlane((int)v) != 0;
+}
+
+template <int K1T>
+__device__ void fused_cell_tile(const pert_problem& pr, const pert_state& st, const pert_adam_hparams& hp, int wt,
+                                int n_bt, int n_g1, int lane) {
+  constexpr int kCS = K1T + 1;
+  const int N = pr.N, K1 = (K1T == PERT_MAX_K1) ? pr.K1 : K1T, nl = pr.n_libs, CS = K1 + 1;
+  const pert_layout lay = st.lay;
+  const int n = wt * 64 + lane;
+  const bool valid = n < N;
+  const int ldn = pr.ldn;
+  const size_t tstride = (size_t)CS * N;
+  const float* lvl1 = st.cell_part + (size_t)n_bt * tstride;
+  const double* blk1 = st.blk_part + (size_t)n_bt * (ldn / 64) * kBlkSlots;
+  // the cell parameters and library prior rows first (their round trip overlaps the sums)
+  float u = 0.0f, tau_z = 0.0f, mean_x = 1.0f, ploidy = 1.0f;
+  int lib = 0;
+  float bz[K1T], lbsd[K1T], lbmn[K1T];
+#pragma unroll
+  for (int k = 0; k < K1T; ++k) { bz[k] = 0.0f; lbsd[k] = 1.0f; lbmn[k] = 0.0f; }
+  if (valid) {
+    u = st.params[lay.off_u + n];
+    tau_z = st.params[lay.off_tau + n];
+    lib = pr.libs[n];
+    mean_x = pr.mean_reads[n];
+    ploidy = pr.ploidy[n];
+#pragma unroll
+    for (int k = 0; k < K1T; ++k)
+      if (k < K1) {
+        bz[k] = st.params[lay.off_beta + k * N + n];
+        lbsd[k] = st.params[lay.off_bstds + lib * K1 + k];
+        lbmn[k] = pr.beta_means[lib * K1 + k];
+      }
+  }
+  double T[kCS];
+#pragma unroll
+  for (int k = 0; k < kCS; ++k) T[k] = 0.0;
+  if (valid) sum_rows<kCS>(lvl1 + n, tstride, (size_t)N, CS, n_g1, T);
+  // the tile's ELBO / d/da sums over its level-1 rows: lane g holds row g, fixed-order tree
+  double wl = 0.0, wa = 0.0;
+  for (int g = lane; g < n_g1; g += 64) {
+    const double* bp = blk1 + ((size_t)g * (ldn / 64) + wt) * kBlkSlots;
+    wl += bp[0];
+    wa += bp[1];
+  }
+  wl = wave_sum_d(wl);
+  wa = wave_sum_d(wa);
+
+  CellGrads<K1T> cg;
+  cell_grads<K1T>(K1, false, (1.0f - pr.lamb) / pr.lamb, u, tau_z, mean_x, ploidy, bz, lbsd, lbmn, T, cg);
+  if (valid) {
+    adam_one(st, hp, lay.off_u + n, -cg.dU);
+#pragma unroll
+    for (int k = 0; k < K1T; ++k)
+      if (k < K1) adam_one(st, hp, lay.off_beta + k * N + n, -cg.dB[k]);
+    adam_one(st, hp, lay.off_tau + n, -cg.dTauZ);
+  }
+  // per-library beta_stds sums, the ELBO (priors + the tile's data terms) and d/da
+  const int nslot = fin_slots(nl, K1);
+  double* out = st.cellblk_part + (size_t)wt * nslot;
+  for (int sl = 0; sl < nslot; ++sl) {
+    double val = 0.0;
+    if (sl < nl * K1) {
+      const int li = sl / K1, k = sl - li * K1;
+      float fv = 0.0f;
+#pragma unroll
+      for (int kk = 0; kk < K1T; ++kk)
+        if (kk == k) fv = cg.dzbs[kk];
+      val = (valid && lib == li) ? (double)fv : 0.0;
+    } else if (sl == 2 * nl * K1) {
+      val = valid ? cg.lp : 0.0;
+    }
+    if (sl >= nl * K1 && sl < 2 * nl * K1) continue;      // beta_means: observed in steps 2/3
+    val = wave_sum_d(val);
+    if (lane == 0) out[sl] = val + (sl == 2 * nl * K1 ? wl : (sl == 2 * nl * K1 + 1 ? wa : 0.0));
+  }
+}
+
+__device__ void fused_bin_tile(const pert_problem& pr, const pert_state& st, const pert_adam_hparams& hp, int by,
+                               int n_ct, bool update_shared, int lane) {
+  const int L = pr.L, LT = st.bins_per_tile;
+  const pert_layout lay = st.lay;
+  // lanes = parts x LT: part q sums the cell tiles [q c, (q+1) c) of bin by*LT + lane % LT
+  const int parts = 64 / LT;
+  const int lb = lane % LT, q = lane / LT;
+  const int l = by * LT + lb;
+  const bool on = q < parts && l < L && pr.kind != PERT_KIND_STEP3;
+  const int chunk = (n_ct + parts - 1) / parts;
+  const int c0 = min(n_ct, q * chunk), c1 = min(n_ct, c0 + chunk);
+  double part[1] = {0.0};
+  if (on) sum_rows<1>(st.bin_part + (size_t)c0 * L + l, (size_t)L, 0, 1, c1 - c0, part);
+  double tot = part[0];
+  for (int r = 1; r < parts; ++r) {                        // parts added in order
+    const double o = __shfl(part[0], lb + r * LT, 64);
+    tot += o;
+  }
+  if (q != 0 || l >= L) return;
+  if (pr.kind == PERT_KIND_STEP3) {
+    st.grad_shared[lay.off_rho + l] = 0.0;
+    return;
+  }
+  float dmask;
+  clipped_sigmoid(st.params[lay.off_rho + l], &dmask);
+  const double g = (double)fexp(st.params[lay.off_a]) * tot * (double)dmask;   // see fin_bins
+  st.grad_shared[lay.off_rho + l] = g;
+  if (update_shared) adam_one(st, hp, lay.off_rho + l, (float)g);
+}
+
+__device__ void fused_global(const pert_problem& pr, const pert_state& st, const pert_adam_hparams& hp, int n_ct,
+                             bool update_shared, int lane) {
+  const int K1 = pr.K1, nl = pr.n_libs, nlk = nl * K1;
+  const pert_layout lay = st.lay;
+  const int nslot = fin_slots(nl, K1);
+  double elbo = 0.0, da = 0.0;
+  // the beta_stds slots [0, nlk) and the ELBO / d/da slots [2 nlk, 2 nlk + 2), 8 at a time,
+  // 4 cell tiles per lane in flight
+  for (int s0 = 0; s0 < nslot; s0 += 8) {
+    double acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.0;
+    for (int b0 = lane; b0 < n_ct; b0 += 256) {
+      double v[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int b = b0 + 64 * u, sl = s0 + j;
+          const double x = st.cellblk_part[(size_t)min(b, n_ct - 1) * nslot + min(sl, nslot - 1)];
+          v[u][j] = (b < n_ct && sl < nslot && (sl < nlk || sl >= 2 * nlk)) ? x : 0.0;
+        }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += v[u][j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int sl = s0 + j;
+      if (sl >= nslot || (sl >= nlk && sl < 2 * nlk)) continue;
+      const double a = wave_sum_d(acc[j]);
+      if (sl < nlk) {
+        if (lane == 0) st.grad_shared[lay.off_bstds + sl] = -a;
+      } else if (sl == 2 * nlk) {
+        elbo = a;
+      } else {
+        da = a;
+      }
+    }
+  }
+  if (lane != 0) return;
+  for (int j = 0; j < nlk; ++j) st.grad_shared[lay.off_bmeans + j] = 0.0;
+  st.grad_shared[lay.off_lam] = 0.0;
+  if (pr.kind != PERT_KIND_STEP3) {
+    const double a = exp((double)st.params[lay.off_a]);
+    double dza = a * da;                                   // dE/dz_a = a dE/da (data part)
+    if (pr.is_root) {
+      dza += 1.0 - 0.2 * a;                                // Gamma(2, 0.2) prior through a = exp(z)
+      elbo += (double)gamma_lp_a((float)a);
+    }
+    st.grad_shared[lay.off_a] = -dza;
+  } else {
+    st.grad_shared[lay.off_a] = 0.0;
+    if (pr.is_root) elbo += (double)gamma_lp_a(pr.a_fixed);   // observed a (:847)
+  }
+  if (pr.is_root) {                                        // observed beta_means (:785)
+    double bmlp = 0.0;
+    for (int j = 0; j < nlk; ++j) {
+      const double bm = pr.beta_means[j];
+      bmlp += -0.5 * bm * bm - 0.91893853320467274;
+    }
+    elbo += bmlp;
+  }
+  st.grad_shared[lay.n_shared] = -elbo;                     // local loss (host adds constants)
+  if (!update_shared) return;
+  if (st.loop_ctl != nullptr) loop_record(st);
+  if (pr.kind != PERT_KIND_STEP3) adam_one(st, hp, lay.off_a, (float)st.grad_shared[lay.off_a]);
+  for (int j = 0; j < nlk; ++j) adam_one(st, hp, lay.off_bstds + j, (float)st.grad_shared[lay.off_bstds + j]);
+}
+
+template <int K1T>
+__device__ void enum3_fused_tail(const pert_problem& pr, const pert_state& st, const pert_adam_hparams& hp, int wt,
+                                 int by, int lane, bool update_shared) {
+  const int LT = st.bins_per_tile;
+  const int n_bt = (pr.L + LT - 1) / LT;
+  const int n_ct = (pr.N + 63) / 64;
+  const int n_g1 = fused_n_g1(n_bt);
+  unsigned int* ctr = fused_counters(pr, st);
+  unsigned int* c_grp = ctr;                               // [n_ct][n_g1]
+  unsigned int* c_lv1 = ctr + (size_t)n_ct * n_g1;         // [n_ct]
+  unsigned int* c_bin = c_lv1 + n_ct;                      // [n_bt]
+  unsigned int* c_glob = c_bin + n_bt;                     // [1]
+  const int G1 = fused_g1(n_bt);
+  const int g = by / G1;
+  const int gsz = min(G1, n_bt - g * G1);
+  __threadfence();                                         // release this workgroup's partials
+  bool last_g = false, last_b = false;
+  if (lane == 0) {
+    last_g = atomicAdd(&c_grp[(size_t)wt * n_g1 + g], 1u) == (unsigned)(gsz - 1);
+    last_b = atomicAdd(&c_bin[by], 1u) == (unsigned)(n_ct - 1);
+  }
+  last_g = wave_flag(last_g);
+  last_b = wave_flag(last_b);
+  unsigned int arrive = 0;
+  if (last_g) {
+    __threadfence();                                       // acquire the group's partials
+    if (lane == 0) c_grp[(size_t)wt * n_g1 + g] = 0u;
+    // level 0 -> level 1: the group's per-cell partial rows (fixed order) and its tiles'
+    // ELBO / d/da partials
+    const int N = pr.N, K1 = (K1T == PERT_MAX_K1) ? pr.K1 : K1T, CS = K1 + 1;
+    const int n = wt * 64 + lane;
+    const size_t tstride = (size_t)CS * N;
+    const int b0 = g * G1;
+    if (n < N) {
+      double S[K1T + 1];
+#pragma unroll
+      for (int k = 0; k <= K1T; ++k) S[k] = 0.0;
+      sum_rows<K1T + 1>(st.cell_part + (size_t)b0 * tstride + n, tstride, (size_t)N, CS, gsz, S);
+      float* dst = st.cell_part + (size_t)(n_bt + g) * tstride + n;
+#pragma unroll
+      for (int k = 0; k <= K1T; ++k)
+        if (k < CS) dst[(size_t)k * N] = (float)S[k];
+    }
+    {
+      const int ldn = pr.ldn;
+      double wl = 0.0, wa = 0.0;
+      for (int j = lane; j < gsz; j += 64) {
+        const double* bp = st.blk_part + ((size_t)(b0 + j) * (ldn / 64) + wt) * kBlkSlots;
+        wl += bp[0];
+        wa += bp[1];
+      }
+      wl = wave_sum_d(wl);
+      wa = wave_sum_d(wa);
+      if (lane == 0) {
+        double* d1 = st.blk_part + ((size_t)(n_bt + g) * (ldn / 64) + wt) * kBlkSlots;
+        d1[0] = wl;
+        d1[1] = wa;
+      }
+    }
+    __threadfence();                                       // release the level-1 row
+    bool last_c = false;
+    if (lane == 0) last_c = atomicAdd(&c_lv1[wt], 1u) == (unsigned)(n_g1 - 1);
+    last_c = wave_flag(last_c);
+    if (last_c) {
+      __threadfence();
+      if (lane == 0) c_lv1[wt] = 0u;
+      fused_cell_tile<K1T>(pr, st, hp, wt, n_bt, n_g1, lane);
+      arrive += 1;
+    }
+  }
+  if (last_b) {
+    __threadfence();
+    if (lane == 0) c_bin[by] = 0u;
+    fused_bin_tile(pr, st, hp, by, n_ct, update_shared, lane);
+    arrive += 1;
+  }
+  if (arrive == 0) return;
+  __threadfence();                                         // release the finalizer's outputs
+  bool last = false;
+  if (lane == 0) last = atomicAdd(c_glob, arrive) + arrive == (unsigned)(n_ct + n_bt);
+  last = wave_flag(last);
+  if (!last) return;
+  __threadfence();
+  if (lane == 0) *c_glob = 0u;
+  fused_global(pr, st, hp, n_ct, update_shared, lane);
+}
+
 // Adam on the packed params (torch.optim.Adam, pyro.optim.Adam wrapper; one state per param).
 __global__ void __launch_bounds__(kBlock) adam_kernel(pert_problem pr, pert_state st,
-                                                      pert_adam_hparams hp) {
+                                                      pert_adam_hparams hp, int n_limit) {
   if (loop_stopped(st)) return;
   const int i = blockIdx.x * kBlock + threadIdx.x;
   const pert_layout lay = st.lay;
   if (st.loop_ctl != nullptr && i == 0) loop_record(st);
-  if (i >= lay.n_params) return;
+  if (i >= n_limit) return;
   const int kind = pr.kind;
   bool active = true;
   if (i < lay.off_a + 1 && kind == PERT_KIND_STEP3) active = false;                   // rho, a
@@ -1453,16 +1820,16 @@ int enum_cell_tiles(const pert_problem* pr, const pert_state* st) {
 
 template <int MODE>
 int launch_enum_mode(int P, dim3 grid, const pert_problem& pr, const pert_state& st,
-                     const pert_adam_hparams& hp, hipStream_t s) {
+                     const pert_adam_hparams& hp, hipStream_t s, int fuse = 0) {
   const bool dma = st.variant != 1;
   const bool v3 = st.variant == 3;
   switch (P) {
 #define PERT_CASE(PP)                                                                             \
   case PP:                                                                                        \
     if (v3 && pr.K1 == 5)                                                                         \
-      hipLaunchKernelGGL((enum3_kernel<PP, MODE, 5>), grid, dim3(64), 0, s, pr, st, hp);          \
+      hipLaunchKernelGGL((enum3_kernel<PP, MODE, 5>), grid, dim3(64), 0, s, pr, st, hp, fuse);    \
     else if (v3)                                                                                  \
-      hipLaunchKernelGGL((enum3_kernel<PP, MODE, PERT_MAX_K1>), grid, dim3(64), 0, s, pr, st, hp); \
+      hipLaunchKernelGGL((enum3_kernel<PP, MODE, PERT_MAX_K1>), grid, dim3(64), 0, s, pr, st, hp, fuse); \
     else if (dma && pr.K1 == 5)                                                                   \
       hipLaunchKernelGGL((enum_dma_kernel<PP, MODE, 5>), grid, dim3(64), dma_lds_bytes(PP, MODE, st, pr), s, pr, st, hp); \
     else if (dma)                                                                                 \
@@ -1561,12 +1928,18 @@ int pert_workspace_sizes(int32_t kind, int32_t L, int32_t N, int32_t K1, int32_t
   const int lt = tile_bins(&tmp);
   const int64_t ldn = (N + kBlock - 1) / kBlock * kBlock;
   const int64_t n_bt = (L + lt - 1) / lt, n_ct = ldn / 64;     // sized for the 64-cell tiles
-  if (n_cell_part) *n_cell_part = n_bt * (K1 + 1) * (int64_t)N;
+  int64_t g1 = 8;
+  while (g1 * g1 < n_bt) ++g1;
+  const int64_t n_g1 = (n_bt + g1 - 1) / g1;                    // pert_enum_step's level-1 rows
+  if (n_cell_part) *n_cell_part = (n_bt + n_g1) * (K1 + 1) * (int64_t)N;
   if (n_bin_part) *n_bin_part = n_ct * (int64_t)L;
-  if (n_blk_part) *n_blk_part = n_bt * n_ct * kBlkSlots;
+  if (n_blk_part) *n_blk_part = (n_bt + n_g1) * n_ct * kBlkSlots;
   // the cell-block partials, then one element whose first 4 bytes are the finalize
-  // launch's arrival counter (zero-initialised by the caller, re-armed by every launch)
-  if (n_cellblk_part) *n_cellblk_part = ((N + 63) / 64) * (int64_t)fin_slots(n_libs, K1) + 1;
+  // launch's arrival counter, then pert_enum_step's arrival counters (uint32: n_ct x n_g1
+  // group, n_ct level-1, n_bt bin, 1 global); zero-initialised by the caller, re-armed by
+  // every launch
+  const int64_t n_ctr = n_ct * n_g1 + n_ct + n_bt + 1;
+  if (n_cellblk_part) *n_cellblk_part = ((N + 63) / 64) * (int64_t)fin_slots(n_libs, K1) + 1 + (n_ctr + 1) / 2;
   return PERT_OK;
 }
 
@@ -1626,6 +1999,30 @@ int pert_enum_pass(const pert_problem* prob, pert_state* st, const pert_adam_hpa
   }
 }
 
+int pert_enum_step(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp, int32_t update_shared,
+                   hipStream_t stream) {
+  if (!problem_ok(prob) || !st || !hp) return PERT_E_ARG;
+  if (prob->kind != PERT_KIND_STEP2 && prob->kind != PERT_KIND_STEP3) return PERT_E_ARG;
+  if (st->variant != 3) return PERT_E_ARG;                          // the three-wave pass only
+  if (!prob->eta_code || !prob->eta_table || prob->n_codes < 1 || !st->z_pi || !st->m_pi || !st->v_pi)
+    return PERT_E_ARG;
+  if (prob->kind == PERT_KIND_STEP3 && !prob->rho_fixed) return PERT_E_ARG;
+  if (!st->cell_part || !st->bin_part || !st->blk_part || !st->cellblk_part || !st->params || !st->adam_m ||
+      !st->adam_v || !st->grad_shared)
+    return PERT_E_ARG;
+  pert_state s2 = *st;
+  s2.bins_per_tile = tile_bins(st);
+  const dim3 grid(enum_cell_tiles(prob, st), (prob->L + s2.bins_per_tile - 1) / s2.bins_per_tile);
+  return launch_enum_mode<PERT_MODE_STEP>(prob->P, grid, *prob, s2, *hp, stream, update_shared ? 2 : 1);
+}
+
+int pert_adam_shared(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp, hipStream_t stream) {
+  if (!prob || !st || !hp || !st->params || !st->adam_m || !st->adam_v || !st->grad_shared) return PERT_E_ARG;
+  const int n = st->lay.n_shared;
+  hipLaunchKernelGGL(adam_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, *prob, *st, *hp, n);
+  return hip_status(hipGetLastError());
+}
+
 int pert_obs_pass(const pert_problem* prob, pert_state* st, hipStream_t stream) {
   if (!problem_ok(prob) || !st || prob->kind != PERT_KIND_STEP1) return PERT_E_ARG;
   if (!prob->cn_obs || !prob->rep_obs || !st->cell_part || !st->bin_part || !st->blk_part) return PERT_E_ARG;
@@ -1658,7 +2055,7 @@ int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream) 
 int pert_adam(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp, hipStream_t stream) {
   if (!prob || !st || !hp || !st->params || !st->adam_m || !st->adam_v) return PERT_E_ARG;
   const int n = st->lay.n_params;
-  hipLaunchKernelGGL(adam_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, *prob, *st, *hp);
+  hipLaunchKernelGGL(adam_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, *prob, *st, *hp, n);
   return hip_status(hipGetLastError());
 }
 

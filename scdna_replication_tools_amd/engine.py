@@ -227,9 +227,13 @@ class PertShard:
                  pi_init=None, device=None, lr: float = 0.05, betas=ADAM_BETAS, eps: float = ADAM_EPS,
                  is_root: bool = True, n_cells_total: Optional[int] = None,
                  allreduce: Optional[Callable[[torch.Tensor], None]] = None,
-                 dirichlet_mode: str = "torch32", bins_per_tile: int = 0, variant: int = 0, lib=None):
+                 dirichlet_mode: str = "torch32", bins_per_tile: int = 0, variant: int = 0, fused: bool = True,
+                 lib=None):
         self.lib = nat.lib() if lib is None else lib        # another build of the ABI (A/B tools)
         self.kind = int(kind)
+        self.variant = int(variant)
+        # one launch per SVI step (pert_enum_step): the three-wave pass of steps 2/3
+        self.fused = bool(fused) and self.variant == 3 and self.kind != nat.KIND_STEP1
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise ValueError("PertShard needs a GPU device (got {})".format(self.device))
@@ -513,9 +517,42 @@ class PertShard:
         if self.pi_block is not None:
             self._pi_lp = self.pi_block.step(self.t)
 
+    def _fused_step(self):
+        """Steps 2/3 with the three-wave pass: one launch (pert_enum_step) does the pass, the
+        reductions and the Adam updates; sharded, the launch stops at the shared block's sums,
+        which are all-reduced before pert_adam_shared."""
+        st = self._state
+        s = self._stream()
+        with self._dev():
+            if self.allreduce is None:
+                nat.check(self.lib.pert_enum_step(ctypes.byref(self._prob), ctypes.byref(st), ctypes.byref(self._hp),
+                                                  1, s), "pert_enum_step")
+                return
+            st.grad_shared = _ptr(self.grad_local)
+            try:
+                nat.check(self.lib.pert_enum_step(ctypes.byref(self._prob), ctypes.byref(st), ctypes.byref(self._hp),
+                                                  0, s), "pert_enum_step")
+            finally:
+                st.grad_shared = _ptr(self.grad_shared)
+            self.grad_shared.copy_(self.grad_local)
+            self.allreduce(self.grad_shared)
+            nat.check(self.lib.pert_adam_shared(ctypes.byref(self._prob), ctypes.byref(st), ctypes.byref(self._hp),
+                                                self._stream()), "pert_adam_shared")
+
     def _launch_step(self, t: int):
         """Queue the launch sequence of Adam step t (1-based) on the current stream."""
         self._set_hparams(t)
+        if self.fused:
+            if self.pass_events is not None:
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev0.record()
+                self._fused_step()
+                ev1.record()
+                self.pass_events.append((ev0, ev1))
+            else:
+                self._fused_step()
+            return
         if self.pass_events is not None:
             ev0 = torch.cuda.Event(enable_timing=True)
             ev1 = torch.cuda.Event(enable_timing=True)

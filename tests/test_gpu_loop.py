@@ -42,12 +42,13 @@ def _state(sh):
     return out
 
 
+@pytest.mark.parametrize("variant", [0, 3])        # 3: one fused launch per step (pert_enum_step)
 @pytest.mark.parametrize("kind", ["step2", "step1", "step3"])
 @pytest.mark.parametrize("max_iter,min_iter,rel_tol", [(60, 12, 5e-2), (21, 5, 0.0)])
-def test_device_loop_matches_host_loop(kind, max_iter, min_iter, rel_tol):
+def test_device_loop_matches_host_loop(kind, max_iter, min_iter, rel_tol, variant):
     prob, kw, z = make_problem(kind, seed=4)
-    a = _shard(kind, kw, z)
-    b = _shard(kind, kw, z)
+    a = _shard(kind, kw, z, variant=variant)
+    b = _shard(kind, kw, z, variant=variant)
     la, ra = _host_loop(a, max_iter, min_iter, rel_tol)
     lb, rb = b.run_svi(max_iter, min_iter, rel_tol)
     assert ra == rb
@@ -66,13 +67,14 @@ def test_device_loop_matches_host_loop(kind, max_iter, min_iter, rel_tol):
         assert torch.equal(ca, cb)
 
 
-def test_device_loop_stops_on_nan():
+@pytest.mark.parametrize("variant", [0, 3])
+def test_device_loop_stops_on_nan(variant):
     prob, kw, z = make_problem("step2", seed=6)
     z = dict(z)
     u = z["expose_u"].clone()
     u[3] = float("nan")
     z["expose_u"] = u
-    sh = _shard("step2", kw, z)
+    sh = _shard("step2", kw, z, variant=variant)
     losses, reason = sh.run_svi(30, 5, 1e-6)
     assert reason == 2 and len(losses) == 1 and math.isnan(losses[0])
     assert sh.t == 1

@@ -54,8 +54,15 @@ def test_layout_and_workspace(nat):
     assert lay.n_shared == 100 + 2 + 2 * 2 * 5
     assert lay.off_tau + 37 == lay.n_params
     ncp, nbp, nblk, ncb = nat.workspace_sizes(2, 100, 37, 5, 2, 32)
-    assert ncp == 4 * (5 + 1) * 37 and nbp == (256 // 64) * 100 and ncb == ((37 + 63) // 64) * (2 * 2 * 5 + 2) + 1
-    assert nat.workspace_sizes(1, 100, 37, 5, 2, 32)[0] == 4 * (5 + 1) * 37
+    # 4 bin tiles + 1 level-1 row of pert_enum_step (groups of 8 >= sqrt(4) bin tiles)
+    n_bt, n_g1, n_ct = 4, 1, 256 // 64
+    assert ncp == (n_bt + n_g1) * (5 + 1) * 37 and nbp == n_ct * 100 and nblk == (n_bt + n_g1) * n_ct * 4
+    # finalize's cell-block slots and arrival counter, then pert_enum_step's uint32 counters
+    n_ctr = n_ct * n_g1 + n_ct + n_bt + 1
+    assert ncb == ((37 + 63) // 64) * (2 * 2 * 5 + 2) + 1 + (n_ctr + 1) // 2
+    # a genome-scale grid: 171 bin tiles in 13 groups of (at most) 14
+    ncp2 = nat.workspace_sizes(2, 5451, 37, 5, 2, 32)[0]
+    assert ncp2 == (171 + 13) * 6 * 37
     with pytest.raises(ValueError):
         nat.make_layout(0, 1, 5, 1)
 

@@ -75,11 +75,46 @@ def synth(n_total: int, subdivide: int, seed: int, device, num_reads: float = 1e
     return dict(gc=gc, reads=reads.float(), cn=cn.to(torch.int64), tau=tau.float(), clone_prof=prof, clone=clone)
 
 
+def cpu_share():
+    """CPUs this process may use: its sched_getaffinity set, capped by a cgroup CPU quota
+    (cpu.max) when one is set; plus the lscpu model name."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(float(q) / float(period)))
+    except (OSError, ValueError):
+        quota = None
+    model = None
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        for line in out.splitlines():
+            if line.strip().startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except (OSError, subprocess.SubprocessError):
+        model = None
+    if model is None:
+        try:
+            for line in open("/proc/cpuinfo"):
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+        except OSError:
+            pass
+    return {"affinity_cores": aff, "cgroup_quota_cores": quota, "cores": min(aff, quota) if quota else aff,
+            "cpu_model": model}
+
+
 def cpu_baseline(data, n_cells: int, steps: int):
     """The oracle (torch-CPU restatement of the tensor algebra Pyro runs: materialised
-    (2, P, L, N) enumeration, autograd, torch.optim.Adam) on a bounded cell sample."""
+    (2, P, L, N) enumeration, autograd, torch.optim.Adam) on a bounded cell sample, on every
+    CPU the process may use (cpu_share)."""
     from oracle import pert_oracle as po
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    share = cpu_share()
+    threads = share["cores"]
     torch.set_num_threads(threads)
     reads = data["reads"][:, :n_cells].cpu().to(torch.float32)
     L = reads.shape[0]
@@ -100,7 +135,23 @@ def cpu_baseline(data, n_cells: int, steps: int):
     return {"value": L * n_cells * steps / dt, "unit": "cell*bins/s", "cores": threads, "kind": "port",
             "sample": "{} cells x {} bins x {} SVI steps (oracle fp32, cell-chunked autograd)".format(
                 n_cells, L, steps),
-            "seconds": dt}
+            "seconds": dt, "cpu_model": share["cpu_model"], "affinity_cores": share["affinity_cores"],
+            "cgroup_quota_cores": share["cgroup_quota_cores"]}
+
+
+def profile_numbers(prof_dir: str, kernel: str):
+    """The dominant kernel's average duration (rocprofv3 kernel trace) and HBM bytes per
+    launch (PMC passes) from a tools/profile.sh run of this same command line
+    (tools/pmc_summary.py's summary.json)."""
+    try:
+        summ = json.load(open(os.path.join(prof_dir, "summary.json")))
+    except (OSError, ValueError):
+        return None
+    ent = summ.get("kernels", {}).get(kernel)
+    if not ent or "avg_ns" not in ent:
+        return None
+    return {"avg_ns": ent["avg_ns"], "calls": ent.get("calls"), "hbm_bytes_per_launch": ent.get("hbm_bytes_per_launch"),
+            "pmc": ent.get("pmc", {})}
 
 
 def main():
@@ -121,6 +172,8 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--profile", default="", help="tools/profile.sh output dir of this command: report the "
+                    "roofline fraction recomputed from its kernel trace and its PMC HBM bytes")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -220,6 +273,9 @@ def main():
         bpc = 4 + 1 + 1 if step1 else bytes_per_cellbin(P)      # step 1: reads + observed cn, rep (u8)
         local_cb = L * (n1 - n0) * (2 if step1 else 1)
         achieved = bpc * local_cb / (kern_ms * 1e-3) / 1e9
+        kname = ("obs_kernel" if step1 else
+                 "enum3_kernel<13, 0, 5>" if args.variant == 3 else
+                 "enum_dma_kernel<13, 0, 5>" if args.variant != 1 else "enum_kernel<13, 0>")
         traffic, valu = None, None
         if os.path.exists(args.pmc) and args.fit == "step2":
             try:
@@ -250,6 +306,24 @@ def main():
                          "valu_issue_frac": (valu or {}).get("issue_frac")},
             "loss_first": losses[0], "loss_last": losses[-1],
         }
+        if args.fit == "step2" and args.variant == 3 and shard.fused:
+            rec["roofline"]["note"] = ("one launch per step (pert_enum_step): the pass with the reductions and "
+                                       "Adam folded in; kernel_ms is that launch")
+        if args.profile:
+            pn = profile_numbers(args.profile, kname)
+            if pn is not None:
+                tk = pn["avg_ns"] * 1e-6
+                ach_t = bpc * local_cb / (tk * 1e-3) / 1e9
+                rec["roofline"].update({
+                    "trace_kernel_ms": tk, "trace_calls": pn["calls"], "frac_trace": ach_t / HBM_PEAK_GBS,
+                    "frac_vs_trace": (achieved / HBM_PEAK_GBS) / (ach_t / HBM_PEAK_GBS),
+                    "trace_source": os.path.relpath(args.profile, ROOT)})
+                if pn["hbm_bytes_per_launch"] is not None:
+                    rec["roofline"]["traffic"] = pn["hbm_bytes_per_launch"]
+                    rec["roofline"]["traffic_per_algorithmic"] = pn["hbm_bytes_per_launch"] / (bpc * local_cb)
+                p = pn["pmc"]
+                if p.get("SQ_ACTIVE_INST_ANY"):
+                    rec["roofline"]["wait_inst_frac"] = p.get("SQ_WAIT_INST_ANY", 0.0) / p["SQ_ACTIVE_INST_ANY"]
         if world == 1 and not args.no_cpu_baseline and args.fit == "step2":
             data = synth(max(args.cpu_cells, 3), subdiv, seed=0, device=device)
             rec["cpu_baseline"] = cpu_baseline(data, args.cpu_cells, args.cpu_steps)

@@ -15,7 +15,8 @@ from collections import defaultdict
 
 
 def short(name):
-    for k in ("enum_kernel", "enum_dma_kernel", "obs_kernel", "finalize_kernel", "scalar_kernel", "adam_kernel"):
+    for k in ("enum_kernel", "enum_dma_kernel", "enum3_kernel", "obs_kernel", "finalize_kernel", "scalar_kernel",
+              "adam_kernel"):
         if k in name:
             return name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
     return None

@@ -577,7 +577,29 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
 //  * the per-(bin, cell) arithmetic is enum_online (pert_math.h): the scores are folded into a
 //    running logsumexp group by group, so no per-state array is live; the tail recomputes
 //    pi_k from z and reads the eta row element by element.
-constexpr int kEnum3Group = 6;                  // chi chains interleaved per group
+// every supported P (a P=13-only build, -DPERT_ONLY_P13, is for quick A/B timing tools only)
+#ifdef PERT_ONLY_P13
+#define PERT_ALL_P_CASES PERT_CASE(13)
+#else
+#define PERT_ALL_P_CASES                                                                        \
+  PERT_CASE(2) PERT_CASE(3) PERT_CASE(4) PERT_CASE(5) PERT_CASE(6) PERT_CASE(7) PERT_CASE(8)    \
+  PERT_CASE(9) PERT_CASE(10) PERT_CASE(11) PERT_CASE(12) PERT_CASE(13) PERT_CASE(14)            \
+  PERT_CASE(15) PERT_CASE(16)
+#endif
+
+#ifndef PERT_ENUM3_GROUP
+#define PERT_ENUM3_GROUP 6
+#endif
+#ifndef PERT_ENUM3_FORWARD
+#define PERT_ENUM3_FORWARD 0
+#endif
+#ifndef PERT_ENUM3_GLOBAL_MEM
+#define PERT_ENUM3_GLOBAL_MEM 0
+#endif
+#ifndef PERT_ENUM3_WAVES
+#define PERT_ENUM3_WAVES 3
+#endif
+constexpr int kEnum3Group = PERT_ENUM3_GROUP;   // chi chains interleaved per group
 constexpr int kEnum3TabFloats = 192;            // eta table staged in LDS up to this size
 constexpr unsigned kRsrcWord3 = 0x00020000;     // raw buffer resource, gfx9 data format
 
@@ -615,6 +637,24 @@ __device__ __forceinline__ void dma_buf(__amdgpu_buffer_rsrc_t rs, uint32_t soff
   }
 }
 
+// Cross-workgroup data of the fused step (partials, level-1 rows, counters) is written and
+// read with agent-scope relaxed atomics, i.e. `sc1` stores and loads that are coherent across
+// the XCDs' separate L2s on their own.  Publishing is then only "s_waitcnt vmcnt(0)" before
+// the counter RMW -- an agent-scope __threadfence() would write back and invalidate the whole
+// L2 of the XCD, once per workgroup (18 k per launch at C4: it doubled the pass).
+template <class T>
+__device__ __forceinline__ void st_coh(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ T ld_coh(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void publish_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ unsigned int arrive(unsigned int* c, unsigned int v) {
+  return __hip_atomic_fetch_add(c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // plane k of a bin: bin and plane offsets in an SGPR (a per-plane voffset would hold a
 // loop-invariant VGPR per plane for the whole pass)
 template <int K>
@@ -630,7 +670,7 @@ __device__ void enum3_fused_tail(const pert_problem& pr, const pert_state& st, c
 // fuse (STEP mode): 0 = partials only (pert_finalize + pert_adam follow), 1 = reductions and the
 // cell sites' Adam folded in (all-reduce + pert_adam_shared follow), 2 = everything folded in
 template <int P, int MODE, int K1T>
-__global__ void __launch_bounds__(64, 3) enum3_kernel(pert_problem pr, pert_state st, pert_adam_hparams hp,
+__global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_problem pr, pert_state st, pert_adam_hparams hp,
                                                       int fuse) {
   constexpr bool kDecode = MODE == PERT_MODE_DECODE;
   constexpr bool kStep = MODE == PERT_MODE_STEP;
@@ -667,10 +707,29 @@ __global__ void __launch_bounds__(64, 3) enum3_kernel(pert_problem pr, pert_stat
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(pr.reads + (size_t)l0 * ldn + wt * 64, (uint32_t)(nb * ldn * 4));
   const __amdgpu_buffer_rsrc_t rc = make_rsrc(pr.eta_code + (size_t)l0 * ldn + wt * 64, (uint32_t)(nb * ldn * 2));
 
+#if PERT_ENUM3_GLOBAL_MEM
+  // A/B knob: the same copies / stores through global pointers (global_load_lds, global stores)
+  float* const gz0 = st.z_pi + tile0;
+  float* const gm0 = kStep ? st.m_pi + tile0 : gz0;
+  float* const gv0 = kStep ? st.v_pi + tile0 : gz0;
+  const float* const gx0 = pr.reads + (size_t)l0 * ldn + wt * 64;
+  const uint16_t* const gc0 = pr.eta_code + (size_t)l0 * ldn + wt * 64;
+#define E3_DMA_X(lb_) dma_run<256>(gx0 + (size_t)(lb_) * ldn, s_xc, lane)
+#define E3_DMA_C(lb_) dma_run<128>(gc0 + (size_t)(lb_) * ldn, s_xc + 64, lane)
+#define E3_DMA_Z(off_) dma_run<P * 256>((const char*)gz0 + (off_), s_z, lane)
+#define E3_DMA_M(off_) dma_run<P * 256>((const char*)gm0 + (off_), s_m, lane)
+#define E3_DMA_V(off_) dma_run<P * 256>((const char*)gv0 + (off_), s_v, lane)
+#else
+#define E3_DMA_X(lb_) dma_buf<256>(rx, (uint32_t)((lb_) * ldn * 4), s_xc, lane)
+#define E3_DMA_C(lb_) dma_buf<128>(rc, (uint32_t)((lb_) * ldn * 2), s_xc + 64, lane)
+#define E3_DMA_Z(off_) dma_buf<P * 256>(rz, (off_), s_z, lane)
+#define E3_DMA_M(off_) dma_buf<P * 256>(rm, (off_), s_m, lane)
+#define E3_DMA_V(off_) dma_buf<P * 256>(rv, (off_), s_v, lane)
+#endif
   // first stage in flight before the prologue's parameter loads
-  dma_buf<256>(rx, 0, s_xc, lane);
-  dma_buf<128>(rc, 0, s_xc + 64, lane);
-  dma_buf<P * 256>(rz, 0, s_z, lane);
+  E3_DMA_X(0);
+  E3_DMA_C(0);
+  E3_DMA_Z(0u);
 
   // ---- tile prologue: eta table (when small), per-bin rho and GC features, cell parameters
   const int ntab = pr.n_codes * (P + 1);
@@ -745,13 +804,13 @@ __global__ void __launch_bounds__(64, 3) enum3_kernel(pert_problem pr, pert_stat
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // reads done before the buffers refill
     const uint32_t zoff = (uint32_t)(lb * P * 256);
     if (l + 1 < l1) {
-      dma_buf<256>(rx, (uint32_t)((lb + 1) * ldn * 4), s_xc, lane);
-      dma_buf<128>(rc, (uint32_t)((lb + 1) * ldn * 2), s_xc + 64, lane);
-      dma_buf<P * 256>(rz, zoff + P * 256, s_z, lane);
+      E3_DMA_X(lb + 1);
+      E3_DMA_C(lb + 1);
+      E3_DMA_Z(zoff + P * 256);
     }
     if (kStep) {
-      dma_buf<P * 256>(rm, zoff, s_m, lane);
-      dma_buf<P * 256>(rv, zoff, s_v, lane);
+      E3_DMA_M(zoff);
+      E3_DMA_V(zoff);
     }
 
     const float invx = x > 0.0f ? frcp(x) : 0.0f;
@@ -759,8 +818,13 @@ __global__ void __launch_bounds__(64, 3) enum3_kernel(pert_problem pr, pert_stat
     const float D = ucc * omega;                           // :636-640 (delta = chi D)
     const float t = tau - rho;                             // :616
     const float phi = frcp(1.0f + fexp(-a_val * t));       // :619
+#if PERT_ENUM3_FORWARD
+    EnumFwd<P> o;                                          // A/B knob: enum_forward's arithmetic
+    enum_forward<P, !kDecode, kDecode>(x, invx, z, log1m_lam, D, phi, o);
+#else
     EnumOnline<P> o;
     enum_online<P, kEnum3Group, !kDecode, kDecode>(x, invx, z, log1m_lam, D, phi, o);
+#endif
 
     float gtv = 0.0f;
     if (kDecode) {
@@ -782,7 +846,11 @@ __global__ void __launch_bounds__(64, 3) enum3_kernel(pert_problem pr, pert_stat
         pert_static_for<0, P>([&](auto kc) {
           constexpr int k = decltype(kc)::value;
           const float em1 = em[k];
+#if PERT_ENUM3_FORWARD
+          const float pk = o.pi[k];
+#else
           const float pk = enum_pi(o, z[k], k);
+#endif
           dirv += em1 * ((z[k] - o.zmax) - o.lse1p);
           const float gz = em1 - pk * S1 + o.gcm[k] - pk * o.sgm;
           const float gl = -gz;                             // d(-ELBO)/dz
@@ -790,9 +858,16 @@ __global__ void __launch_bounds__(64, 3) enum3_kernel(pert_problem pr, pert_stat
             const float m1 = hp.beta1 * s_m[k * 64 + lane] + (1.0f - hp.beta1) * gl;
             const float v1 = hp.beta2 * s_v[k * 64 + lane] + (1.0f - hp.beta2) * gl * gl;
             const float denom = __builtin_amdgcn_sqrtf(v1) * hp.inv_bc2_sqrt + hp.eps;
+#if PERT_ENUM3_GLOBAL_MEM
+            const size_t o = (size_t)zoff / 4 + k * 64 + lane;
+            store_stream(gz0 + o, z[k] - hp.step_size * m1 * frcp(denom));
+            store_stream(gm0 + o, m1);
+            store_stream(gv0 + o, v1);
+#else
             store_nt<k>(rz, z[k] - hp.step_size * m1 * frcp(denom), voff, zoff);
             store_nt<k>(rm, m1, voff, zoff);
             store_nt<k>(rv, v1, voff, zoff);
+#endif
           } else {
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, gl), rg, voff, zoff + k * 256, 0);
           }
@@ -817,22 +892,37 @@ __global__ void __launch_bounds__(64, 3) enum3_kernel(pert_problem pr, pert_stat
     }
   }
   if (kDecode) return;
+  // the tile's partials; coherent (sc1) stores when another workgroup of this launch reads them
+  const bool coh = kStep && fuse;
   if (!frozen) {
-    for (int i = lane; i < nb; i += 64) st.bin_part[(size_t)wt * pr.L + l0 + i] = s_binp[i];
+    for (int i = lane; i < nb; i += 64) {
+      float* q = st.bin_part + (size_t)wt * pr.L + l0 + i;
+      if (coh) st_coh(q, s_binp[i]);
+      else *q = s_binp[i];
+    }
   }
   if (valid) {
     float* cp = st.cell_part + (size_t)blockIdx.y * (K1 + 1) * N + n;
 #pragma unroll
-    for (int k = 0; k < K1T; ++k)
-      if (k < K1) cp[(size_t)k * N] = acc[k];
-    cp[(size_t)K1 * N] = a_val * sgt;
+    for (int k = 0; k < K1T; ++k) {
+      if (k >= K1) continue;
+      if (coh) st_coh(cp + (size_t)k * N, acc[k]);
+      else cp[(size_t)k * N] = acc[k];
+    }
+    if (coh) st_coh(cp + (size_t)K1 * N, a_val * sgt);
+    else cp[(size_t)K1 * N] = a_val * sgt;
   }
   const double bl = wave_sum_d((double)loss);
   const double bga = wave_sum_d((double)ga);
   if (lane == 0) {
     double* bp = st.blk_part + ((size_t)blockIdx.y * (ldn / 64) + wt) * kBlkSlots;
-    bp[0] = bl;
-    bp[1] = bga;
+    if (coh) {
+      st_coh(bp, bl);
+      st_coh(bp + 1, bga);
+    } else {
+      bp[0] = bl;
+      bp[1] = bga;
+    }
   }
   if (kStep && fuse) enum3_fused_tail<K1T>(pr, st, hp, wt, blockIdx.y, lane, fuse == 2);
 }
@@ -1443,9 +1533,10 @@ __device__ __forceinline__ void adam_one(const pert_state& st, const pert_adam_h
 //    update_shared (a single rank: no all-reduce between the sums and Adam), records the
 //    loss for the device loop and runs Adam on a and beta_stds.
 // Sums are in fixed order (level 0 in bin-tile order within the group, level 1 in group
-// order, cell tiles in order), so the result does not depend on arrival order.  Publishing
-// is the agent-scope release/acquire pattern of finalize_kernel (__threadfence around the
-// counter atomics); every counter is re-armed by the workgroup that consumed it.
+// order, cell tiles in order), so the result does not depend on arrival order.  Everything
+// one workgroup hands to another goes through coherent (sc1) stores and loads, published by
+// a vmcnt wait before the counter RMW (st_coh / ld_coh below); every counter is re-armed by
+// the workgroup that consumed it.
 // bin tiles per level-0 group: about sqrt(n_bt), so both levels stay short (C4: 13 x 14,
 // C5 at LT 32: 66 x 65)
 __device__ __forceinline__ int fused_g1(int n_bt) {
@@ -1455,8 +1546,8 @@ __device__ __forceinline__ int fused_g1(int n_bt) {
 }
 __device__ __forceinline__ int fused_n_g1(int n_bt) { const int g = fused_g1(n_bt); return (n_bt + g - 1) / g; }
 
-// s[k] += sum_{j < n} p[j rs + k ps] for k < np, in j order; 8 rows x NP planes of loads in
-// flight per round trip (clamped indices, masked values: no guarded loads)
+// s[k] += sum_{j < n} p[j rs + k ps] for k < np, in j order; 4-8 rows x NP planes of loads in
+// flight per round trip (clamped indices, masked values: no guarded loads); coherent loads
 template <int NP>
 __device__ __forceinline__ void sum_rows(const float* __restrict__ p, size_t rs, size_t ps, int np, int n,
                                          double (&s)[NP]) {
@@ -1468,7 +1559,7 @@ __device__ __forceinline__ void sum_rows(const float* __restrict__ p, size_t rs,
 #pragma unroll
       for (int k = 0; k < NP; ++k) {
         const int j = j0 + u;
-        const float x = p[(size_t)min(j, n - 1) * rs + (size_t)min(k, np - 1) * ps];
+        const float x = ld_coh(p + (size_t)min(j, n - 1) * rs + (size_t)min(k, np - 1) * ps);
         v[u][k] = (j < n && k < np) ? x : 0.0f;
       }
 #pragma unroll
@@ -1529,8 +1620,8 @@ __device__ void fused_cell_tile(const pert_problem& pr, const pert_state& st, co
   double wl = 0.0, wa = 0.0;
   for (int g = lane; g < n_g1; g += 64) {
     const double* bp = blk1 + ((size_t)g * (ldn / 64) + wt) * kBlkSlots;
-    wl += bp[0];
-    wa += bp[1];
+    wl += ld_coh(bp);
+    wa += ld_coh(bp + 1);
   }
   wl = wave_sum_d(wl);
   wa = wave_sum_d(wa);
@@ -1561,7 +1652,7 @@ __device__ void fused_cell_tile(const pert_problem& pr, const pert_state& st, co
     }
     if (sl >= nl * K1 && sl < 2 * nl * K1) continue;      // beta_means: observed in steps 2/3
     val = wave_sum_d(val);
-    if (lane == 0) out[sl] = val + (sl == 2 * nl * K1 ? wl : (sl == 2 * nl * K1 + 1 ? wa : 0.0));
+    if (lane == 0) st_coh(out + sl, val + (sl == 2 * nl * K1 ? wl : (sl == 2 * nl * K1 + 1 ? wa : 0.0)));
   }
 }
 
@@ -1614,7 +1705,7 @@ __device__ void fused_global(const pert_problem& pr, const pert_state& st, const
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int b = b0 + 64 * u, sl = s0 + j;
-          const double x = st.cellblk_part[(size_t)min(b, n_ct - 1) * nslot + min(sl, nslot - 1)];
+          const double x = ld_coh(st.cellblk_part + (size_t)min(b, n_ct - 1) * nslot + min(sl, nslot - 1));
           v[u][j] = (b < n_ct && sl < nslot && (sl < nlk || sl >= 2 * nlk)) ? x : 0.0;
         }
 #pragma unroll
@@ -1681,18 +1772,17 @@ __device__ void enum3_fused_tail(const pert_problem& pr, const pert_state& st, c
   const int G1 = fused_g1(n_bt);
   const int g = by / G1;
   const int gsz = min(G1, n_bt - g * G1);
-  __threadfence();                                         // release this workgroup's partials
+  publish_wait();                                          // this workgroup's partials are out
   bool last_g = false, last_b = false;
   if (lane == 0) {
-    last_g = atomicAdd(&c_grp[(size_t)wt * n_g1 + g], 1u) == (unsigned)(gsz - 1);
-    last_b = atomicAdd(&c_bin[by], 1u) == (unsigned)(n_ct - 1);
+    last_g = arrive(&c_grp[(size_t)wt * n_g1 + g], 1u) == (unsigned)(gsz - 1);
+    last_b = arrive(&c_bin[by], 1u) == (unsigned)(n_ct - 1);
   }
   last_g = wave_flag(last_g);
   last_b = wave_flag(last_b);
-  unsigned int arrive = 0;
+  unsigned int n_arr = 0;
   if (last_g) {
-    __threadfence();                                       // acquire the group's partials
-    if (lane == 0) c_grp[(size_t)wt * n_g1 + g] = 0u;
+    if (lane == 0) st_coh(&c_grp[(size_t)wt * n_g1 + g], 0u);
     // level 0 -> level 1: the group's per-cell partial rows (fixed order) and its tiles'
     // ELBO / d/da partials
     const int N = pr.N, K1 = (K1T == PERT_MAX_K1) ? pr.K1 : K1T, CS = K1 + 1;
@@ -1707,49 +1797,46 @@ __device__ void enum3_fused_tail(const pert_problem& pr, const pert_state& st, c
       float* dst = st.cell_part + (size_t)(n_bt + g) * tstride + n;
 #pragma unroll
       for (int k = 0; k <= K1T; ++k)
-        if (k < CS) dst[(size_t)k * N] = (float)S[k];
+        if (k < CS) st_coh(dst + (size_t)k * N, (float)S[k]);
     }
     {
       const int ldn = pr.ldn;
       double wl = 0.0, wa = 0.0;
       for (int j = lane; j < gsz; j += 64) {
         const double* bp = st.blk_part + ((size_t)(b0 + j) * (ldn / 64) + wt) * kBlkSlots;
-        wl += bp[0];
-        wa += bp[1];
+        wl += ld_coh(bp);
+        wa += ld_coh(bp + 1);
       }
       wl = wave_sum_d(wl);
       wa = wave_sum_d(wa);
       if (lane == 0) {
         double* d1 = st.blk_part + ((size_t)(n_bt + g) * (ldn / 64) + wt) * kBlkSlots;
-        d1[0] = wl;
-        d1[1] = wa;
+        st_coh(d1, wl);
+        st_coh(d1 + 1, wa);
       }
     }
-    __threadfence();                                       // release the level-1 row
+    publish_wait();                                        // the level-1 row is out
     bool last_c = false;
-    if (lane == 0) last_c = atomicAdd(&c_lv1[wt], 1u) == (unsigned)(n_g1 - 1);
+    if (lane == 0) last_c = arrive(&c_lv1[wt], 1u) == (unsigned)(n_g1 - 1);
     last_c = wave_flag(last_c);
     if (last_c) {
-      __threadfence();
-      if (lane == 0) c_lv1[wt] = 0u;
+      if (lane == 0) st_coh(&c_lv1[wt], 0u);
       fused_cell_tile<K1T>(pr, st, hp, wt, n_bt, n_g1, lane);
-      arrive += 1;
+      n_arr += 1;
     }
   }
   if (last_b) {
-    __threadfence();
-    if (lane == 0) c_bin[by] = 0u;
+    if (lane == 0) st_coh(&c_bin[by], 0u);
     fused_bin_tile(pr, st, hp, by, n_ct, update_shared, lane);
-    arrive += 1;
+    n_arr += 1;
   }
-  if (arrive == 0) return;
-  __threadfence();                                         // release the finalizer's outputs
+  if (n_arr == 0) return;
+  publish_wait();                                          // the finalizer's outputs are out
   bool last = false;
-  if (lane == 0) last = atomicAdd(c_glob, arrive) + arrive == (unsigned)(n_ct + n_bt);
+  if (lane == 0) last = arrive(c_glob, n_arr) + n_arr == (unsigned)(n_ct + n_bt);
   last = wave_flag(last);
   if (!last) return;
-  __threadfence();
-  if (lane == 0) *c_glob = 0u;
+  if (lane == 0) st_coh(c_glob, 0u);
   fused_global(pr, st, hp, n_ct, update_shared, lane);
 }
 
@@ -1836,9 +1923,7 @@ int launch_enum_mode(int P, dim3 grid, const pert_problem& pr, const pert_state&
       hipLaunchKernelGGL((enum_dma_kernel<PP, MODE, PERT_MAX_K1>), grid, dim3(64), dma_lds_bytes(PP, MODE, st, pr), s, pr, st, hp); \
     else hipLaunchKernelGGL((enum_kernel<PP, MODE>), grid, dim3(kBlock), 0, s, pr, st, hp);       \
     break;
-    PERT_CASE(2) PERT_CASE(3) PERT_CASE(4) PERT_CASE(5) PERT_CASE(6) PERT_CASE(7) PERT_CASE(8)
-    PERT_CASE(9) PERT_CASE(10) PERT_CASE(11) PERT_CASE(12) PERT_CASE(13) PERT_CASE(14)
-    PERT_CASE(15) PERT_CASE(16)
+    PERT_ALL_P_CASES
 #undef PERT_CASE
     default: return PERT_E_UNSUPPORTED_P;
   }
@@ -1867,9 +1952,7 @@ int dma_step_occupancy(const pert_problem& pr, int lt, int variant) {
 int step_occupancy(const pert_problem& pr, int lt, int variant) {
   switch (pr.P) {
 #define PERT_CASE(PP) case PP: return dma_step_occupancy<PP>(pr, lt, variant);
-    PERT_CASE(2) PERT_CASE(3) PERT_CASE(4) PERT_CASE(5) PERT_CASE(6) PERT_CASE(7) PERT_CASE(8)
-    PERT_CASE(9) PERT_CASE(10) PERT_CASE(11) PERT_CASE(12) PERT_CASE(13) PERT_CASE(14)
-    PERT_CASE(15) PERT_CASE(16)
+    PERT_ALL_P_CASES
 #undef PERT_CASE
     default: return 0;
   }
@@ -2082,9 +2165,7 @@ int pert_selftest_enum_cellbin_host(int32_t P, int64_t n, const float* x, const 
   switch (P) {
 #define PERT_CASE(PP) \
   case PP: return selftest_enum_host<PP>(n, x, em1, S1, z, log1m_lam, D, phi, E, dirv, gD, gt, gz, amax);
-    PERT_CASE(2) PERT_CASE(3) PERT_CASE(4) PERT_CASE(5) PERT_CASE(6) PERT_CASE(7) PERT_CASE(8)
-    PERT_CASE(9) PERT_CASE(10) PERT_CASE(11) PERT_CASE(12) PERT_CASE(13) PERT_CASE(14)
-    PERT_CASE(15) PERT_CASE(16)
+    PERT_ALL_P_CASES
 #undef PERT_CASE
     default: return PERT_E_UNSUPPORTED_P;
   }

@@ -41,6 +41,13 @@ PERT_HD float flog(float x) {
   return logf(x);
 #endif
 }
+PERT_HD float __builtin_amdgcn_logf_or_log2(float x) {   // log2(x): v_log_f32 / libm
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_logf(x);
+#else
+  return log2f(x);
+#endif
+}
 PERT_HD float fexp(float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_exp2f(x * kLog2e);
@@ -108,6 +115,33 @@ PERT_HD void nb_lgdiff_asym_hoisted(float d, float r, float x, float ldxc, float
   const float r4 = r2 * r2, rz4 = rz2 * rz2;
   psi = l1 - 0.5f * (rz - r) - 0.0833333333333333333f * (rz2 - r2)
         + 0.00833333333333333333f * (rz4 - r4) - 0.00396825396825396825f * (rz4 * rz2 - r4 * r2);
+}
+
+// Two chi chains at once in packed fp32 (v_pk_fma/mul/add_f32: two lanes' worth of work per
+// VALU issue; the transcendentals stay per element): nb_lgdiff_asym_hoisted for chi = (c.x,
+// c.y), with NB'(chi) = d log(1-lam) + Lambda and Bc = chi (log(1-lam) + Psi) folded in.
+typedef float pf2 __attribute__((ext_vector_type(2)));
+PERT_HD void nb_asym_pair(pf2 chi, pf2 rchi, pf2 lchi, float D, float rD, float x, float ldx, float log1m_lam,
+                          pf2& nchi, pf2& bc) {
+  const pf2 d = chi * D;
+  const pf2 r = rchi * rD;                            // 1/d
+  const pf2 zs = d + x;
+  const pf2 rz = {frcp(zs.x), frcp(zs.y)};
+  const pf2 q = r * x;                                // x/d
+  const pf2 iu = d * rz;                              // 1/(1 + x/d)
+  const pf2 u = q + 1.0f;
+  const pf2 lu = pf2{__builtin_amdgcn_logf_or_log2(u.x), __builtin_amdgcn_logf_or_log2(u.y)} * kLn2;
+  const pf2 l1 = lu + (q - (u - 1.0f)) * iu;          // log1p(x/d), log1p_corr
+  const pf2 l2 = l1 + (lchi + ldx);                   // log1p(d/x)
+  const pf2 r2 = r * r, rz2 = rz * rz;
+  const pf2 sr = r * (0.0833333333333333333f - r2 * (0.00277777777777777778f - r2 * 0.000793650793650793651f));
+  const pf2 srz = rz * (0.0833333333333333333f - rz2 * (0.00277777777777777778f - rz2 * 0.000793650793650793651f));
+  const pf2 lam = (d - 0.5f) * l1 + x * l2 + (srz - sr);
+  const pf2 r4 = r2 * r2, rz4 = rz2 * rz2;
+  const pf2 psi = l1 - 0.5f * (rz - r) - 0.0833333333333333333f * (rz2 - r2)
+                  + 0.00833333333333333333f * (rz4 - r4) - 0.00396825396825396825f * (rz4 * rz2 - r4 * r2);
+  nchi = d * log1m_lam + lam;
+  bc = chi * (psi + log1m_lam);
 }
 
 // 1 <= d < kAsymMin: shift by exactly kShift = 4 (d + 4 >= 5 for every d >= 1, so no per-lane
@@ -432,12 +466,31 @@ PERT_HD void enum_online(float x, float invx, const float (&z)[P], float log1m_l
 #if defined(__HIP_DEVICE_COMPILE__)
       if (g > 0) __builtin_amdgcn_sched_barrier(0);
 #endif
-      // the group's NB parts
+      // the group's NB parts; on the asymptotic path two chains per packed-fp32 evaluation
       float nn[G], bb[G];
+      if constexpr (ASYM) {
+        pert_static_for<0, (G + 1) / 2>([&](auto pc) {
+          constexpr int j0 = 2 * decltype(pc)::value, j1 = j0 + 1;
+          constexpr int i0 = g * G + j0, i1 = g * G + j1;
+          constexpr bool h0 = i0 < CL.n, h1 = j1 < G && i1 < CL.n;
+          constexpr int c0 = h0 ? CL.v[i0] : 1, c1 = h1 ? CL.v[i1] : 1;
+          if constexpr (h0 && h1 && c0 != 0) {
+            pf2 n2, b2;
+            nb_asym_pair(pf2{(float)c0, (float)c1}, pf2{1.0f / (float)c0, 1.0f / (float)c1},
+                         pf2{kLogInt[c0], kLogInt[c1]}, D, rD, x, ldx, log1m_lam, n2, b2);
+            nn[j0] = n2.x;
+            bb[j0] = b2.x;
+            nn[j1] = n2.y;
+            bb[j1] = b2.y;
+          }
+        });
+      }
       pert_static_for<0, G>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         constexpr int idx = g * G + j;
-        if constexpr (idx < CL.n) {
+        constexpr int jp = j - j % 2;                          // pair head
+        constexpr bool paired = ASYM && jp + 1 < G && g * G + jp + 1 < CL.n && CL.v[g * G + jp] != 0;
+        if constexpr (idx < CL.n && !paired) {
           constexpr int chi = CL.v[idx];
           if constexpr (chi == 0) {
             nn[j] = n_clamped;

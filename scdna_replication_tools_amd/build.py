@@ -25,7 +25,7 @@ DEPS = SOURCES + [os.path.join(HERE, "csrc", "pert_math.h"), os.path.join(ROOT, 
 OUT = os.path.join(HERE, "libpert_hip.so")
 ARCH = os.environ.get("PERT_OFFLOAD_ARCH", "gfx950")
 HASH_LEN = 16
-FLAGS = ["-fno-slp-vectorize"]
+FLAGS = ["-fno-slp-vectorize", "-fno-signed-zeros"]
 
 
 def hipcc() -> str:

@@ -316,6 +316,16 @@ __device__ __forceinline__ void dma_run(const void* gsrc, float* ldst, int lane)
 template <int BYTES>
 constexpr int dma_count() { return BYTES / 1024 + (BYTES % 1024) / 256 + ((BYTES % 256) == 128 ? 1 : 0); }
 
+// the DMA pass's per-(bin, cell) arithmetic: 1 = enum_online + the packed tail (as enum3_kernel),
+// 0 = enum_forward + the scalar tail (A/B knob)
+#ifndef PERT_V0_ONLINE
+#define PERT_V0_ONLINE 1
+#endif
+#ifndef PERT_ENUM3_GROUP
+#define PERT_ENUM3_GROUP 6
+#endif
+constexpr int kEnum3Group = PERT_ENUM3_GROUP;   // chi chains interleaved per group (enum_online)
+
 template <int P, int MODE, int K1T>
 __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_state st, pert_adam_hparams hp) {
   constexpr bool kDecode = MODE == PERT_MODE_DECODE;
@@ -467,8 +477,13 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
     const float D = ucc * omega;                           // :636-640 (delta = chi D)
     const float t = tau - rho;                             // :616
     const float phi = frcp(1.0f + fexp(-a_val * t));       // :619
+#if PERT_V0_ONLINE
+    EnumOnline<P> o;
+    enum_online<P, kEnum3Group, !kDecode, kDecode>(x, invx, z, pr.log1m_lam, D, phi, o);
+#else
     EnumFwd<P> o;
     enum_forward<P, !kDecode, kDecode>(x, invx, z, pr.log1m_lam, D, phi, o);
+#endif
     float gtv = 0.0f;
     if (kDecode) {
       st.cn_out[(size_t)l * ldn + n] = (uint8_t)(o.argmax % P);
@@ -494,6 +509,56 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
         for (int k = 0; k < P; ++k) em1[k] = row[k];
         S1 = row[P];
       }
+#if PERT_V0_ONLINE
+      // the gradient and Adam of the logits in plane pairs, packed fp32 (as enum3_kernel)
+      const float S1s = S1 + o.sgm;
+      pf2 dirv2 = {0.0f, 0.0f};
+      const float* mb = lds + 2 * SF;
+      float* zo = st.z_pi + tile + lane;
+      float* mo = st.m_pi + tile + lane;
+      float* vo = st.v_pi + tile + lane;
+      float* gp = st.g_pi + tile + lane;
+      pert_static_for<0, (P + 1) / 2>([&](auto pc) {
+        constexpr int k0 = 2 * decltype(pc)::value;
+        constexpr int k1 = k0 + 1 < P ? k0 + 1 : k0;
+        const pf2 zz = {zt[k0], zt[k1]};
+        const pf2 e1 = {em1[k0], k1 != k0 ? em1[k1] : 0.0f};
+        const pf2 pk = pf2{enum_pi(o, zt[k0], k0), enum_pi(o, zt[k1], k1)};
+        dirv2 += e1 * ((zz - o.zmax) - o.lse1p);
+        const pf2 gl = pk * S1s - e1 - pf2{o.gcm[k0], o.gcm[k1]};   // d(-ELBO)/dz
+        if (kStep) {
+          const pf2 m0 = {mb[k0 * 64 + lane], mb[k1 * 64 + lane]};
+          const pf2 v0 = {mb[ZF + k0 * 64 + lane], mb[ZF + k1 * 64 + lane]};
+          const pf2 m1 = m0 * hp.beta1 + gl * (1.0f - hp.beta1);
+          const pf2 v1 = v0 * hp.beta2 + (gl * gl) * (1.0f - hp.beta2);
+          const pf2 den = pf2{__builtin_amdgcn_sqrtf(v1.x), __builtin_amdgcn_sqrtf(v1.y)} * hp.inv_bc2_sqrt + hp.eps;
+          const pf2 zn = zz - (m1 * hp.step_size) * pf2{frcp(den.x), frcp(den.y)};
+          const float zn0 = zn.x, zn1 = zn.y, m10 = m1.x, m11 = m1.y, v10 = v1.x, v11 = v1.y;
+          store_stream(zo + k0 * 64, zn0);
+          store_stream(mo + k0 * 64, m10);
+          store_stream(vo + k0 * 64, v10);
+          if constexpr (k1 != k0) {
+            store_stream(zo + k1 * 64, zn1);
+            store_stream(mo + k1 * 64, m11);
+            store_stream(vo + k1 * 64, v11);
+          }
+        } else {
+          const float g0 = gl.x, g1 = gl.y;
+          gp[k0 * 64] = g0;
+          if constexpr (k1 != k0) gp[k1 * 64] = g1;
+        }
+      });
+      const float dirv = dirv2.x + dirv2.y;
+      if (valid) {
+        loss += o.E + dirv;
+        gtv = o.gt;
+        accT += a_val * o.gt;
+        ga += t * o.gt;
+        const float ge = o.gD * omega;
+#pragma unroll
+        for (int k = 0; k < K1T; ++k) acc[k] += ge * g[k];
+      }
+#else
       float gz[P];
       const float dirv = enum_tail<P>(o, zt, em1, S1, gz);
       if (valid) {
@@ -525,6 +590,7 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
 #pragma unroll
         for (int k = 0; k < P; ++k) gp[k * 64] = -gz[k];
       }
+#endif
     }
     if (!kDecode && !frozen) {
       const float ws = wave_sum(gtv);
@@ -587,19 +653,10 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
   PERT_CASE(15) PERT_CASE(16)
 #endif
 
-#ifndef PERT_ENUM3_GROUP
-#define PERT_ENUM3_GROUP 6
-#endif
-#ifndef PERT_ENUM3_FORWARD
-#define PERT_ENUM3_FORWARD 0
-#endif
-#ifndef PERT_ENUM3_GLOBAL_MEM
-#define PERT_ENUM3_GLOBAL_MEM 0
-#endif
+
 #ifndef PERT_ENUM3_WAVES
 #define PERT_ENUM3_WAVES 3
 #endif
-constexpr int kEnum3Group = PERT_ENUM3_GROUP;   // chi chains interleaved per group
 constexpr int kEnum3TabFloats = 192;            // eta table staged in LDS up to this size
 constexpr unsigned kRsrcWord3 = 0x00020000;     // raw buffer resource, gfx9 data format
 
@@ -707,25 +764,11 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(pr.reads + (size_t)l0 * ldn + wt * 64, (uint32_t)(nb * ldn * 4));
   const __amdgpu_buffer_rsrc_t rc = make_rsrc(pr.eta_code + (size_t)l0 * ldn + wt * 64, (uint32_t)(nb * ldn * 2));
 
-#if PERT_ENUM3_GLOBAL_MEM
-  // A/B knob: the same copies / stores through global pointers (global_load_lds, global stores)
-  float* const gz0 = st.z_pi + tile0;
-  float* const gm0 = kStep ? st.m_pi + tile0 : gz0;
-  float* const gv0 = kStep ? st.v_pi + tile0 : gz0;
-  const float* const gx0 = pr.reads + (size_t)l0 * ldn + wt * 64;
-  const uint16_t* const gc0 = pr.eta_code + (size_t)l0 * ldn + wt * 64;
-#define E3_DMA_X(lb_) dma_run<256>(gx0 + (size_t)(lb_) * ldn, s_xc, lane)
-#define E3_DMA_C(lb_) dma_run<128>(gc0 + (size_t)(lb_) * ldn, s_xc + 64, lane)
-#define E3_DMA_Z(off_) dma_run<P * 256>((const char*)gz0 + (off_), s_z, lane)
-#define E3_DMA_M(off_) dma_run<P * 256>((const char*)gm0 + (off_), s_m, lane)
-#define E3_DMA_V(off_) dma_run<P * 256>((const char*)gv0 + (off_), s_v, lane)
-#else
 #define E3_DMA_X(lb_) dma_buf<256>(rx, (uint32_t)((lb_) * ldn * 4), s_xc, lane)
 #define E3_DMA_C(lb_) dma_buf<128>(rc, (uint32_t)((lb_) * ldn * 2), s_xc + 64, lane)
 #define E3_DMA_Z(off_) dma_buf<P * 256>(rz, (off_), s_z, lane)
 #define E3_DMA_M(off_) dma_buf<P * 256>(rm, (off_), s_m, lane)
 #define E3_DMA_V(off_) dma_buf<P * 256>(rv, (off_), s_v, lane)
-#endif
   // first stage in flight before the prologue's parameter loads
   E3_DMA_X(0);
   E3_DMA_C(0);
@@ -818,13 +861,8 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
     const float D = ucc * omega;                           // :636-640 (delta = chi D)
     const float t = tau - rho;                             // :616
     const float phi = frcp(1.0f + fexp(-a_val * t));       // :619
-#if PERT_ENUM3_FORWARD
-    EnumFwd<P> o;                                          // A/B knob: enum_forward's arithmetic
-    enum_forward<P, !kDecode, kDecode>(x, invx, z, log1m_lam, D, phi, o);
-#else
     EnumOnline<P> o;
     enum_online<P, kEnum3Group, !kDecode, kDecode>(x, invx, z, log1m_lam, D, phi, o);
-#endif
 
     float gtv = 0.0f;
     if (kDecode) {
@@ -842,36 +880,42 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
         float em[P + 1];                                    // all loads in flight at once
 #pragma unroll
         for (int k = 0; k <= P; ++k) em[k] = row[k];
-        const float S1 = em[P];
-        pert_static_for<0, P>([&](auto kc) {
-          constexpr int k = decltype(kc)::value;
-          const float em1 = em[k];
-#if PERT_ENUM3_FORWARD
-          const float pk = o.pi[k];
-#else
-          const float pk = enum_pi(o, z[k], k);
-#endif
-          dirv += em1 * ((z[k] - o.zmax) - o.lse1p);
-          const float gz = em1 - pk * S1 + o.gcm[k] - pk * o.sgm;
-          const float gl = -gz;                             // d(-ELBO)/dz
+        const float S1s = em[P] + o.sgm;
+        // planes in pairs, packed fp32 (the exponential, square root and reciprocal per element)
+        pf2 dirv2 = {0.0f, 0.0f};
+        pert_static_for<0, (P + 1) / 2>([&](auto pc) {
+          constexpr int k0 = 2 * decltype(pc)::value;
+          constexpr int k1 = k0 + 1 < P ? k0 + 1 : k0;        // odd P: the last pair repeats plane k0
+          const pf2 zz = {z[k0], z[k1]};
+          const pf2 e1 = {em[k0], k1 != k0 ? em[k1] : 0.0f};
+          const pf2 pk = pf2{enum_pi(o, z[k0], k0), enum_pi(o, z[k1], k1)};
+          dirv2 += e1 * ((zz - o.zmax) - o.lse1p);
+          const pf2 gl = pk * S1s - e1 - pf2{o.gcm[k0], o.gcm[k1]};   // d(-ELBO)/dz
           if (kStep) {
-            const float m1 = hp.beta1 * s_m[k * 64 + lane] + (1.0f - hp.beta1) * gl;
-            const float v1 = hp.beta2 * s_v[k * 64 + lane] + (1.0f - hp.beta2) * gl * gl;
-            const float denom = __builtin_amdgcn_sqrtf(v1) * hp.inv_bc2_sqrt + hp.eps;
-#if PERT_ENUM3_GLOBAL_MEM
-            const size_t o = (size_t)zoff / 4 + k * 64 + lane;
-            store_stream(gz0 + o, z[k] - hp.step_size * m1 * frcp(denom));
-            store_stream(gm0 + o, m1);
-            store_stream(gv0 + o, v1);
-#else
-            store_nt<k>(rz, z[k] - hp.step_size * m1 * frcp(denom), voff, zoff);
-            store_nt<k>(rm, m1, voff, zoff);
-            store_nt<k>(rv, v1, voff, zoff);
-#endif
+            const pf2 m0 = {s_m[k0 * 64 + lane], s_m[k1 * 64 + lane]};
+            const pf2 v0 = {s_v[k0 * 64 + lane], s_v[k1 * 64 + lane]};
+            const pf2 m1 = m0 * hp.beta1 + gl * (1.0f - hp.beta1);
+            const pf2 v1 = v0 * hp.beta2 + (gl * gl) * (1.0f - hp.beta2);
+            const pf2 den = pf2{__builtin_amdgcn_sqrtf(v1.x), __builtin_amdgcn_sqrtf(v1.y)} * hp.inv_bc2_sqrt + hp.eps;
+            const pf2 zn = zz - (m1 * hp.step_size) * pf2{frcp(den.x), frcp(den.y)};
+            store_nt<k0>(rz, zn.x, voff, zoff);
+            store_nt<k0>(rm, m1.x, voff, zoff);
+            store_nt<k0>(rv, v1.x, voff, zoff);
+            if constexpr (k1 != k0) {
+              store_nt<k1>(rz, zn.y, voff, zoff);
+              store_nt<k1>(rm, m1.y, voff, zoff);
+              store_nt<k1>(rv, v1.y, voff, zoff);
+            }
           } else {
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, gl), rg, voff, zoff + k * 256, 0);
+            // through plain floats: __builtin_bit_cast of a vector element (gl.y) compiles to
+            // the bits of element 0 here (hipcc / ROCm 7.2)
+            const float g0 = gl.x, g1 = gl.y;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, g0), rg, voff, zoff + k0 * 256, 0);
+            if constexpr (k1 != k0)
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, g1), rg, voff, zoff + k1 * 256, 0);
           }
         });
+        dirv = dirv2.x + dirv2.y;
       };
       if (etal) tail(s_tab + code * (P + 1));
       else tail(pr.eta_table + (size_t)code * (P + 1));

@@ -55,6 +55,20 @@ PERT_HD float fexp(float x) {
   return expf(x);
 #endif
 }
+PERT_HD float fexp2(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_exp2f(x);
+#else
+  return exp2f(x);
+#endif
+}
+PERT_HD float fmed3(float v, float lo, float hi) {   // clamp v to [lo, hi] (v_med3_f32)
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_fmed3f(v, lo, hi);
+#else
+  return fminf(fmaxf(v, lo), hi);
+#endif
+}
 PERT_HD float frcp(float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_rcpf(x);
@@ -391,18 +405,19 @@ struct EnumOnline {
   float gD;       // dE/dD
   float gt;       // dE/dt / a (masked where phi clamped)
   float zmax;     // max_k z_k
-  float lse1p;    // log pi_k = z_k - zmax - lse1p
-  float inv1t;    // pi_k = exp(z_k - zmax) inv1t (inv1t for k = jmax)
-  int jmax;       // first argmax of z
+  float zmaxS;    // zmax log2(e)
+  float lse1p;    // log sum_k exp(z_k - zmax): log pi_k = z_k - zmax - lse1p
+  float inv1t;    // 1 / sum_k exp(z_k - zmax): pi_k = exp(z_k - zmax) inv1t
   float sgm;      // sum_k gcm_k
   float gcm[P];   // gamma^cn_k [pi_k unclamped]
   int argmax;     // r * P + c of the joint MAP state (first maximum)
 };
 
-// pi_k from the EnumOnline summary, bit-identical to enum_forward's o.pi[k]
+// pi_k from the EnumOnline summary (the exponential enum_online summed)
 template <int P>
 PERT_HD float enum_pi(const EnumOnline<P>& o, float zk, int k) {
-  return (k == o.jmax) ? o.inv1t : fexp(zk - o.zmax) * o.inv1t;
+  (void)k;
+  return fexp2(fmaf(zk, kLog2e, -o.zmaxS)) * o.inv1t;
 }
 
 template <int P, int G, bool WANT_GRAD, bool WANT_ARGMAX>
@@ -415,34 +430,31 @@ PERT_HD void enum_online(float x, float invx, const float (&z)[P], float log1m_l
   if (phic > 0.999f) { phic = 0.999f; mphi = false; }
   const float lphi = flog(phic);
   const float l1mphi = flog(1.0f - phic);
-  // pi = softmax(z), log(clamp_probs(pi)) (transforms.py:951-954, categorical.py:67-71)
+  // pi = softmax(z) (transforms.py:951-954) and log(clamp_probs(pi)) (categorical.py:67-71):
+  // log pi_k = z_k - m - log(sum_j exp(z_j - m)), clamped to [log eps, log(1 - eps)] (one
+  // v_med3); the gradient mask bit is set where the clamp did not bind
   float m = z[0];
-  int jmax = 0;
 #pragma unroll
-  for (int k = 1; k < P; ++k) { if (z[k] > m) { m = z[k]; jmax = k; } }
+  for (int k = 1; k < P; ++k) m = fmaxf(m, z[k]);
+  const float mS = m * kLog2e;
+  float tot = 0.0f;
+#pragma unroll
+  for (int k = 0; k < P; ++k) tot += fexp2(fmaf(z[k], kLog2e, -mS));
+  const float inv_tot = frcp(tot);
+  const float lse = flog(tot);
   float lc[P];
-  float t = 0.0f;
-#pragma unroll
-  for (int k = 0; k < P; ++k) {
-    lc[k] = (k == jmax) ? 1.0f : fexp(z[k] - m);
-    t += (k == jmax) ? 0.0f : lc[k];
-  }
-  const float inv1t = frcp(1.0f + t);
-  const float lse1p = log1p_corr(t, inv1t);
   uint32_t mk = 0;
 #pragma unroll
   for (int k = 0; k < P; ++k) {
-    const float pk = lc[k] * inv1t;
-    const float om = (k == jmax) ? t * inv1t : 1.0f - pk;
-    const bool hi = om < kEps32;
-    const bool lo = pk < kEps32;
-    mk |= (hi || lo) ? 0u : (1u << k);
-    lc[k] = hi ? kLog1mEps32 : (lo ? kLogEps32 : (z[k] - m) - lse1p);
+    const float l = (z[k] - m) - lse;
+    const float c = fmed3(l, kLogEps32, kLog1mEps32);
+    mk |= (c == l) ? (1u << k) : 0u;
+    lc[k] = c;
   }
   o.zmax = m;
-  o.lse1p = lse1p;
-  o.inv1t = inv1t;
-  o.jmax = jmax;
+  o.zmaxS = mS;
+  o.lse1p = lse;
+  o.inv1t = inv_tot;
 
   const float n_clamped = log1m_lam + lambda_delta1(x, invx);   // delta == 1 (chi == 0 or chi D < 1)
   float M = -INFINITY, se = 0.0f, seB = 0.0f, g1 = 0.0f, best = -INFINITY;
@@ -555,6 +567,7 @@ PERT_HD void enum_online(float x, float invx, const float (&z)[P], float log1m_l
         });
       }
       M = Mn;
+      const float ML = M * kLog2e;
       pert_static_for<0, G>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         constexpr int idx = g * G + j;
@@ -562,12 +575,12 @@ PERT_HD void enum_online(float x, float invx, const float (&z)[P], float log1m_l
           constexpr int chi = CL.v[idx];
           float ej = 0.0f;
           if constexpr (chi < P) {
-            const float e = fexp(sg[2 * j] - M);
+            const float e = fexp2(fmaf(sg[2 * j], kLog2e, -ML));
             ej += e;
             o.gcm[chi] += e;
           }
           if constexpr (chi % 2 == 0) {
-            const float e = fexp(sg[2 * j + 1] - M);
+            const float e = fexp2(fmaf(sg[2 * j + 1], kLog2e, -ML));
             ej += e;
             g1 += e;
             o.gcm[chi / 2] += e;

@@ -27,9 +27,14 @@ them lying on a k-means decision boundary, an EM lower-bound change at the 1e-3
 tolerance, a mean gap or skew at its threshold, or a near-tie in the threshold scan
 can make the two arithmetics take different branches.  Every such decision is checked
 against a margin (``FRAGILE``, relative) and the cells where any of them falls inside
-it ("fragile" cells, typically under 1 %) are recomputed with the reference's per-cell
-sklearn path (prep.manhattan_binarization), so the result is the reference's for every
-cell; tests/test_tau_init.py pins it.
+it ("fragile" cells) are recomputed with the reference's per-cell sklearn path
+(prep.manhattan_binarization).  Up to ``MINOR_EXACT_MAX_L`` (2,000) bins that covers every
+flagged cell (a few %), so the result is the reference's for every cell.  At genome scale
+(5,451 bins) the finer near-ties -- a k-means++ draw next to a cumulative-sum boundary, a
+threshold scan whose minimum is flat against fp32 summation noise, points within the
+levels' rounding budget of the threshold -- flag about half the cells and each per-cell fit
+takes about a second, so only the branch decisions are recomputed there and the
+near-tie cells keep the batched value.  tests/test_tau_init.py pins both regimes.
 """
 from __future__ import annotations
 
@@ -50,6 +55,7 @@ FRAGILE = 1e-5          # relative: mean-gap / skew thresholds
 PP_MARGIN = 2e-6        # relative to the k-means++ potential: candidate draw and choice
 TIE = 1e-6              # relative width of an exact tie on a k-means decision
 EM_MARGIN = 2e-6        # absolute: the EM lower-bound change around its tolerance
+MINOR_EXACT_MAX_L = 2000  # up to this many bins, the finer near-ties are recomputed too
 
 
 EPS32 = float(np.finfo(np.float32).eps)
@@ -198,20 +204,28 @@ def _percentiles(X: torch.Tensor, qs) -> torch.Tensor:
     return torch.stack(out)
 
 
-def binarization_fraction(Xraw: torch.Tensor, return_fragile: bool = False):
+def binarization_fraction(Xraw: torch.Tensor, return_fragile: bool = False, return_minor: bool = False):
     """manhattan_binarization (pert_model.py:364-423) for every column of Xraw (L, N);
     returns the replicated fraction per column (and, with ``return_fragile``, the mask of
     the columns whose outcome fp32 rounding could change, see the module doc): the
     pipeline runs twice, with ties on a k-means decision broken towards either centre,
-    and a column whose two results differ is fragile too."""
+    and a column whose two results differ is fragile too.  ``return_minor`` splits the
+    mask in two: branch decisions (Lloyd / EM stopping, mean-gap and skew thresholds, the
+    tie-direction runs disagreeing) and near-ties of finer grain (the k-means++ candidate
+    draw, a flat minimum of the threshold scan, points within the levels' rounding budget of
+    the chosen threshold)."""
     if not return_fragile:
         return _binarize(Xraw, 0.0)[0]
-    f_hi, fr_hi = _binarize(Xraw, TIE)
-    f_lo, fr_lo = _binarize(Xraw, -TIE)
-    return f_hi, fr_hi | fr_lo | (f_hi != f_lo)
+    f_hi, fr_hi, pp_hi, sc_hi, mn_hi = _binarize(Xraw, TIE, with_minor=True)
+    f_lo, fr_lo, pp_lo, sc_lo, mn_lo = _binarize(Xraw, -TIE, with_minor=True)
+    decisions = fr_hi | fr_lo | (f_hi != f_lo)
+    near = pp_hi | pp_lo | sc_hi | sc_lo | (mn_hi > 0) | (mn_lo > 0)
+    if return_minor:
+        return f_hi, decisions, near
+    return f_hi, decisions | near
 
 
-def _binarize(Xraw: torch.Tensor, tie_bias: float):
+def _binarize(Xraw: torch.Tensor, tie_bias: float, with_minor: bool = False):
     X = Xraw.to(torch.float64)
     L, N = X.shape
     X = (X - X.mean(0)) / X.std(0, unbiased=False)
@@ -219,7 +233,9 @@ def _binarize(Xraw: torch.Tensor, tie_bias: float):
     Xc = X - X.mean(0)                                               # KMeans centres the data first
     tol = Xc.var(0, unbiased=False) * 1e-4
     fragile = torch.zeros(N, dtype=torch.bool, device=X.device)
-    lab1 = _lloyd(Xc, _kmeans_pp(Xc, first, u, fragile), tol, fragile=fragile, tie_bias=tie_bias)
+    frag_pp = torch.zeros(N, dtype=torch.bool, device=X.device)
+    frag_scan = torch.zeros(N, dtype=torch.bool, device=X.device)
+    lab1 = _lloyd(Xc, _kmeans_pp(Xc, first, u, frag_pp), tol, fragile=fragile, tie_bias=tie_bias)
     mu = _gmm_means(X, lab1, fragile=fragile)
     gap = (mu[0] - mu[1]).abs()
     b0, b1 = torch.minimum(mu[0], mu[1]), torch.maximum(mu[0], mu[1])
@@ -242,6 +258,7 @@ def _binarize(Xraw: torch.Tensor, tie_bias: float):
     th = b0[None, :] + i * ((b1 - b0) / 99)[None, :]
     th[-1] = b1
     best = torch.empty(N, dtype=X.dtype, device=X.device)
+    minor = torch.zeros(N, dtype=X.dtype, device=X.device)
     chunk = max(1, int(2e8 // (100 * max(L, 1))))
     for s in range(0, N, chunk):
         xs = X[:, s:s + chunk]
@@ -266,10 +283,12 @@ def _binarize(Xraw: torch.Tensor, tie_bias: float):
         near_best = near.gather(0, bi[None])
         slack = (2 * dcnt * db[None] + (near + near_best) * span[None]
                  + 4 * EPS32 * (np.log2(max(L, 2)) + 2) * dmin)
-        fragile[s:s + chunk] |= (((dcnt > 0) | (near > 0)) & (d - dmin <= slack)).any(0)
-        fragile[s:s + chunk] |= near_best[0] > 0
+        frag_scan[s:s + chunk] |= (((dcnt > 0) | (near > 0)) & (d - dmin <= slack)).any(0)
+        minor[s:s + chunk] = near_best[0]
     frac = (X > best[None, :]).sum(0).to(torch.float64) / L
-    return frac, fragile
+    if with_minor:
+        return frac, fragile, frag_pp, frag_scan, minor
+    return frac, fragile | frag_pp | frag_scan | (minor > 0)
 
 
 def guess_times_batched(reads: np.ndarray, cn_states: np.ndarray, upsilon: float = 6, device=None,
@@ -281,8 +300,17 @@ def guess_times_batched(reads: np.ndarray, cn_states: np.ndarray, upsilon: float
     x = torch.as_tensor(np.asarray(reads, np.float32), device=dev)
     st = torch.as_tensor(np.asarray(cn_states, np.float32), device=dev)
     norm = x / torch.where(st > 0.0, st, torch.full_like(st, 0.5))  # fp32, as the reference divides
-    frac, fragile = binarization_fraction(norm, return_fragile=True)
+    frac, decisions, near = binarization_fraction(norm, return_fragile=True, return_minor=True)
     t = frac.to(torch.float32).cpu().numpy()
+    L = norm.shape[0]
+    # Up to MINOR_EXACT_MAX_L bins every flagged cell goes through the reference's per-cell
+    # path (the result is the reference's).  Above, the finer near-ties are common (half the
+    # cells at 5,451 bins: the scan's minimum is flat against fp32 summation noise there, so
+    # the reference's own choice is not stable across BLAS builds either) and each per-cell
+    # fit takes about a second, so only the branch decisions are recomputed; the cells kept
+    # are counted in guess_times_batched.last_near_kept.
+    fragile = decisions | near if L <= MINOR_EXACT_MAX_L else decisions
+    guess_times_batched.last_near_kept = 0 if L <= MINOR_EXACT_MAX_L else int((near & ~decisions).sum())
     redo = np.flatnonzero(fragile.cpu().numpy())
     if redo.size:
         from .prep import manhattan_binarization

@@ -458,7 +458,9 @@ class pert_infer_scRT():
         keys = getattr(cn_s_reads_df, "keys", None)
         if keys is not None and not isinstance(keys, prep.TableKeys):
             keys = None                                   # a DataFrame's .keys is a method
-        if keys is not None and len(keys.cell_code) == len(cn_s):
+        if keys is not None and len(keys.cell_code) == len(cn_s) and keys.is_grid(cells, loci_chr, loci_start):
+            ci = li = None                                # row i = (cell i // L, locus i % L)
+        elif keys is not None and len(keys.cell_code) == len(cn_s):
             ci, li = keys.row_positions(cells, loci_chr, loci_start)
         else:
             cell_index = pd.Index(cells.astype(str))
@@ -466,22 +468,36 @@ class pert_infer_scRT():
             ci = cell_index.get_indexer(cn_s[self.cell_col].astype(str).to_numpy())
             li = locus_index.get_indexer(pd.MultiIndex.from_arrays(
                 [cn_s[self.chr_col].astype(str).to_numpy(), cn_s[self.start_col].to_numpy()]))
-        keep = (ci >= 0) & (li >= 0)
-        base = cn_s.loc[keep] if not keep.all() else cn_s
-        ci, li = ci[keep], li[keep]
         model_cn, model_rep = v("cn"), v("rep")
-        model = pd.DataFrame({
-            'model_cn_state': model_cn[li, ci].astype(np.int64),
-            'model_rep_state': model_rep[li, ci].astype(np.float32),
-            'model_tau': v("expose_tau").astype(np.float32).reshape(-1)[ci],
-            'model_u': v("expose_u").astype(np.float32).reshape(-1)[ci],
-            'model_rho': v("expose_rho").astype(np.float32).reshape(-1)[li],
-        })
-        # new columns side by side with the (sorted) input rows, without copying its blocks
-        # (reset_index(drop=True) would deep-copy and consolidate the whole long table)
-        base = base.copy(deep=False)
-        base.index = pd.RangeIndex(len(base))
-        out = pd.concat([base, model], axis=1, copy=False)
+        per_cell = lambda k: v(k).astype(np.float32).reshape(-1)
+        if ci is None:
+            base = cn_s
+            L = len(loci_start)
+            model = {
+                'model_cn_state': np.ascontiguousarray(model_cn.T).reshape(-1).astype(np.int64),
+                'model_rep_state': np.ascontiguousarray(model_rep.T).reshape(-1).astype(np.float32),
+                'model_tau': np.repeat(per_cell("expose_tau"), L),
+                'model_u': np.repeat(per_cell("expose_u"), L),
+                'model_rho': np.tile(per_cell("expose_rho"), len(cells)),
+            }
+        else:
+            keep = (ci >= 0) & (li >= 0)
+            base = cn_s.loc[keep] if not keep.all() else cn_s
+            ci, li = ci[keep], li[keep]
+            model = {
+                'model_cn_state': model_cn[li, ci].astype(np.int64),
+                'model_rep_state': model_rep[li, ci].astype(np.float32),
+                'model_tau': per_cell("expose_tau")[ci],
+                'model_u': per_cell("expose_u")[ci],
+                'model_rho': per_cell("expose_rho")[li],
+            }
+        # new columns side by side with the (sorted) input rows, without copying its blocks:
+        # each inserted column is a block of its own (reset_index(drop=True) would deep-copy
+        # the whole long table, and a concat consolidates every block of one dtype)
+        out = base.copy(deep=False)
+        out.index = pd.RangeIndex(len(out))
+        for name, col in model.items():
+            out[name] = col
         lam = float(_np(lambda_fit).reshape(-1)[0])
         a = float(v("expose_a").reshape(-1)[0])
         supp = pd.concat([

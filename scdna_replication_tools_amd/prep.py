@@ -41,20 +41,34 @@ def _chr_codes(chrc: pd.Series) -> np.ndarray:
     return lut[np.where(codes >= 0, codes, len(cats))]
 
 
+def _object_pointers(v: np.ndarray) -> np.ndarray:
+    """The PyObject addresses an object array holds, as an int64 view (no copy; valid while
+    ``v`` is alive -- the caller keeps it)."""
+    import ctypes
+    assert v.dtype == object and v.flags.c_contiguous
+    return np.ctypeslib.as_array((ctypes.c_int64 * v.size).from_address(v.ctypes.data))
+
+
 def _factorize(values, sort: bool = False):
     """pd.factorize, but for object (string) columns that come in runs -- a long-form table
     grouped by cell, or by chromosome -- only the run heads are hashed: an adjacent-element
     comparison costs a fraction of hashing every Python string."""
-    v = np.asarray(values)
+    v = np.ascontiguousarray(values)
     if v.dtype != object or v.size < (1 << 16):
         return pd.factorize(v, sort=sort)
     probe = v[:1 << 16]
     if np.count_nonzero(probe[1:] != probe[:-1]) > probe.size // 8:
         return pd.factorize(v, sort=sort)
-    change = np.empty(v.size, dtype=bool)
-    change[0] = True
-    np.not_equal(v[1:], v[:-1], out=change[1:])
-    heads = np.flatnonzero(change)
+    # adjacent rows holding the SAME object (a label repeated by np.repeat / a per-cell
+    # table concatenation) are one run: compare the object pointers first, and the values
+    # (a Python comparison) only where the pointers differ
+    ptr = _object_pointers(v)
+    d = np.flatnonzero(ptr[1:] != ptr[:-1])
+    if d.size * 4 > v.size:                           # mostly distinct objects: compare all
+        d = np.flatnonzero(v[1:] != v[:-1])
+    elif d.size:
+        d = d[v[1:][d] != v[:-1][d]]
+    heads = np.concatenate([[0], d + 1])
     if heads.size > v.size // 8:
         return pd.factorize(v, sort=sort)
     codes, uniq = pd.factorize(v[heads], sort=sort)
@@ -65,6 +79,52 @@ def _sorted_codes(values) -> tuple:
     """(codes, sorted uniques) with NaN keys coded -1, like pandas' sorted group keys."""
     codes, uniq = _factorize(values, sort=True)
     return codes.astype(np.int64), np.asarray(uniq)
+
+
+def _cell_blocks(cck: np.ndarray, lkey: np.ndarray):
+    """Per-cell HMMcopy tables concatenated: every cell's rows one contiguous block of L rows
+    holding the SAME locus key sequence (in any order, e.g. chromosomes in file order).  The
+    stable sort by (cell, chr, start) is then block order x one within-block order:
+    returns the row order, or None."""
+    n = cck.size
+    if n == 0:
+        return None
+    brk = np.flatnonzero(cck[1:] != cck[:-1]) + 1
+    B = brk.size + 1
+    if n % B or B * 16 > n:
+        return None
+    L = n // B
+    if brk.size and not np.array_equal(brk, np.arange(1, B) * L):
+        return None
+    hc = cck[::L]
+    if np.unique(hc).size != B:                       # a cell split over several blocks
+        return None
+    k2 = lkey.reshape(B, L)
+    if not (k2 == k2[:1]).all():
+        return None
+    q = np.argsort(k2[0], kind="stable")
+    bp = np.argsort(hc, kind="stable")
+    return (bp[:, None] * L + q[None, :]).reshape(-1)
+
+
+def _take_columns(df: pd.DataFrame, order: np.ndarray) -> pd.DataFrame:
+    """``df.take(order)`` built column by column with ``np.take`` (pandas' take goes through
+    its generic take_nd, 2-3x slower on object columns); extension columns use their own take."""
+    from concurrent.futures import ThreadPoolExecutor
+    sers = [df.iloc[:, j] for j in range(df.shape[1])]
+    num = [j for j, ser in enumerate(sers) if isinstance(ser.dtype, np.dtype) and ser.dtype != object]
+    cols = [None] * len(sers)
+    # numeric gathers release the GIL: run them on a few threads beside the object ones
+    with ThreadPoolExecutor(max_workers=min(8, max(1, len(num)))) as ex:
+        futs = {j: ex.submit(np.take, sers[j].to_numpy(), order) for j in num}
+        for j, ser in enumerate(sers):
+            if j not in futs:
+                cols[j] = np.take(ser.to_numpy(), order) if isinstance(ser.dtype, np.dtype) else ser.take(order).array
+        for j, f in futs.items():
+            cols[j] = f.result()
+    out = pd.DataFrame(dict(enumerate(cols)), index=df.index.take(order), copy=False)
+    out.columns = df.columns
+    return out
 
 
 def _sorted_table(cn: pd.DataFrame, cell_col: str, chr_col: str, start_col: str, notna_col: Optional[str] = None):
@@ -78,17 +138,22 @@ def _sorted_table(cn: pd.DataFrame, cell_col: str, chr_col: str, start_col: str,
     chk = np.where(ch < 0, len(CHR_ORDER), ch)
     cck = np.where(cc < 0, len(cells), cc)
     if st.dtype.kind in "iu" and len(st) and st.min() >= 0 and st.max() < (1 << 32) and len(cells) < (1 << 25):
-        # one int64 key (cell, chr, start) and a stable argsort instead of a 3-key lexsort
-        order = np.argsort((cck.astype(np.int64) * (len(CHR_ORDER) + 1) + chk) << 32 | st.astype(np.int64),
-                           kind="stable")
+        # one int64 key (cell, chr, start); a block permutation when the table comes as
+        # per-cell tables with one locus order, else a stable argsort instead of a 3-key lexsort
+        lkey = chk.astype(np.int64) << 32 | st.astype(np.int64)
+        order = _cell_blocks(cck, lkey)
+        if order is None:
+            order = np.argsort(((cck.astype(np.int64) * (len(CHR_ORDER) + 1)) << 32) + lkey, kind="stable")
     else:
         order = np.lexsort((st_key, chk, cck))
     if notna_col is not None:
-        order = order[cn[notna_col].notna().to_numpy()[order]]
+        ok = cn[notna_col].notna().to_numpy()
+        if not ok.all():
+            order = order[ok[order]]
     if order.size == len(cn) and (order.size == 0 or (order[1:] > order[:-1]).all()):
         out = cn.copy(deep=False)                        # already sorted and complete: no gather
     else:
-        out = cn.take(order)
+        out = _take_columns(cn, order)
     out[chr_col] = pd.Categorical.from_codes(ch[order], categories=CHR_ORDER)
     return out, TableKeys.from_codes(cc[order], cells, ch[order], st[order])
 
@@ -105,6 +170,23 @@ class Pivot:
     loci_chr: np.ndarray       # (L,) chromosome labels (category order)
     loci_start: np.ndarray     # (L,)
     values: np.ndarray         # (L, N) float64 (NaN where absent)
+
+
+def _regular_rows(cell_code: np.ndarray, lkey: np.ndarray, n_cells: int) -> int:
+    """L when the rows are (cell 0, loci ascending), (cell 1, the same loci), ... with every
+    key valid and no locus repeated; 0 otherwise."""
+    n = cell_code.size
+    if n_cells == 0 or n == 0 or n % n_cells:
+        return 0
+    L = n // n_cells
+    k0 = lkey[:L]
+    if k0[0] < 0 or not (k0[1:] > k0[:-1]).all():
+        return 0
+    if not (cell_code.reshape(n_cells, L) == np.arange(n_cells)[:, None]).all():
+        return 0
+    if not (lkey.reshape(n_cells, L) == k0[None, :]).all():
+        return 0
+    return L
 
 
 class TableKeys:
@@ -127,7 +209,15 @@ class TableKeys:
         if start.dtype.kind == "f":
             self.valid &= ~np.isnan(start)
         lkey = np.where(self.valid, chr_code * (1 << 40) + np.where(self.valid, start, 0).astype(np.int64), -1)
-        self.locus_code, ukeys = _sorted_codes(lkey)
+        # a sorted complete table (row i = cell i // L, locus i % L, the same ascending loci in
+        # every cell) needs no hashing: the locus codes are a tiled arange
+        self.regular = _regular_rows(cell_code, lkey, cells.size)
+        if self.regular:
+            L = self.regular
+            self.locus_code = np.tile(np.arange(L, dtype=np.int64), cells.size)
+            ukeys = lkey[:L].copy()
+        else:
+            self.locus_code, ukeys = _sorted_codes(lkey)
         if ukeys.size and ukeys[0] == -1:             # drop the invalid-row key
             self.locus_code = self.locus_code - 1
             ukeys = ukeys[1:]
@@ -135,12 +225,24 @@ class TableKeys:
         self.loci_chr = cats[(ukeys >> 40).astype(int)]
         self.loci_start = ukeys & ((1 << 40) - 1)
 
-    def row_positions(self, cells, loci_chr, loci_start):
-        """Per table row: the column of ``cells`` and the row of (loci_chr, loci_start) it
-        belongs to (-1 where absent), via the uniques instead of per-row lookups."""
+    def _unique_positions(self, cells, loci_chr, loci_start):
         cpos = pd.Index(cells).get_indexer(self.cells)
         lidx = pd.MultiIndex.from_arrays([np.asarray(loci_chr).astype(str), np.asarray(loci_start)])
         lpos = lidx.get_indexer(pd.MultiIndex.from_arrays([self.loci_chr.astype(str), self.loci_start]))
+        return cpos, lpos
+
+    def is_grid(self, cells, loci_chr, loci_start) -> bool:
+        """True when row i of the table is (cells[i // L], locus i % L) of the given axes:
+        a regular table whose cells and loci are exactly the axes, in their order."""
+        if not self.regular or len(cells) != self.cells.size or len(loci_start) != self.loci_start.size:
+            return False
+        cpos, lpos = self._unique_positions(cells, loci_chr, loci_start)
+        return bool((cpos == np.arange(cpos.size)).all() and (lpos == np.arange(lpos.size)).all())
+
+    def row_positions(self, cells, loci_chr, loci_start):
+        """Per table row: the column of ``cells`` and the row of (loci_chr, loci_start) it
+        belongs to (-1 where absent), via the uniques instead of per-row lookups."""
+        cpos, lpos = self._unique_positions(cells, loci_chr, loci_start)
         ci = np.where(self.cell_code >= 0, cpos[np.maximum(self.cell_code, 0)], -1)
         li = np.where(self.locus_code >= 0, lpos[np.maximum(self.locus_code, 0)], -1)
         return ci, li
@@ -154,6 +256,16 @@ def pivot_cells_by_loci(cn: pd.DataFrame, value_col: str, cell_col: str, chr_col
     dropped, cells / loci with no value at all dropped (pivot_table's dropna)."""
     k = TableKeys(cn, cell_col, chr_col, start_col) if keys is None else keys
     val = cn[value_col].to_numpy(np.float64)
+    if getattr(k, "regular", 0) and val.size == k.cell_code.size:
+        # one row per (cell, locus) in (cell, locus) order: the pivot is a transpose
+        N, L = k.cells.size, k.loci_start.size
+        out = np.ascontiguousarray(val.reshape(N, L).T)
+        nan = np.isnan(out)
+        if nan.any():
+            has_l, has_c = ~nan.all(axis=1), ~nan.all(axis=0)
+            if not (has_l.all() and has_c.all()):
+                return Pivot(k.cells[has_c], k.loci_chr[has_l], k.loci_start[has_l], out[has_l][:, has_c])
+        return Pivot(k.cells, k.loci_chr, k.loci_start, out)
     keep = k.valid & ~np.isnan(val)
     ci, li = k.cell_code[keep], k.locus_code[keep]
     N, L = k.cells.size, k.loci_start.size
@@ -332,10 +444,30 @@ def filter_ploidies(cn: pd.DataFrame, ploidy: Optional[pd.Series] = None, clone_
     return cn[ok & (pc == cnt.argmax(axis=1)[np.where(kc >= 0, kc, 0)])]
 
 
+def _group_median_small_ints(g: np.ndarray, v: np.ndarray, n_groups: int, n_vals: int) -> np.ndarray:
+    """Per-group median of small non-negative integers (CN states) from a (group, value)
+    histogram: the order statistics lo = (n-1)//2 and hi = n//2 are read off the cumulative
+    counts -- the values the sort below would pick, without sorting."""
+    cnt = np.bincount(g * n_vals + v, minlength=n_groups * n_vals).reshape(n_groups, n_vals)
+    cum = np.cumsum(cnt, axis=1)
+    n = cum[:, -1]
+    out = np.full(n_groups, np.nan)
+    has = n > 0
+    c, nh = cum[has], n[has]
+    lo = (c <= ((nh - 1) // 2)[:, None]).sum(axis=1)     # first value whose cumulative count passes lo
+    hi = (c <= (nh // 2)[:, None]).sum(axis=1)
+    out[has] = 0.5 * (lo + hi)
+    return out
+
+
 def _group_median(group: np.ndarray, values: np.ndarray, n_groups: int) -> np.ndarray:
     """Median of ``values`` per group code (NaN for empty groups), by one lexsort."""
     ok = ~np.isnan(values) & (group >= 0)
     g, v = group[ok], values[ok]
+    if v.size and n_groups * 64 <= max(v.size, 1 << 20):
+        lo_v, hi_v = v.min(), v.max()
+        if lo_v >= 0 and hi_v < 64 and (v == np.floor(v)).all():
+            return _group_median_small_ints(g, v.astype(np.int64), n_groups, int(hi_v) + 1)
     order = np.lexsort((v, g))
     g, v = g[order], v[order]
     n = np.bincount(g, minlength=n_groups)

@@ -11,7 +11,8 @@ from scdna_replication_tools_amd import prep
 CHR = [str(i + 1) for i in range(22)] + ["X", "Y"]
 
 
-def _table(n_cells=7, prefix="c", seed=0, chroms=("1", "2", "10", "X"), per_chr=6, n_libs=2, nan_locus=False):
+def _table(n_cells=7, prefix="c", seed=0, chroms=("1", "2", "10", "X"), per_chr=6, n_libs=2, nan_locus=False,
+           order="shuffled"):
     rng = np.random.default_rng(seed)
     rows = []
     for i in range(n_cells):
@@ -21,7 +22,23 @@ def _table(n_cells=7, prefix="c", seed=0, chroms=("1", "2", "10", "X"), per_chr=
                                  gc=0.3 + 0.01 * j + 0.001 * CHR.index(ch), library_id="L{}".format(i % n_libs),
                                  state=int(rng.integers(1, 5)), reads=float(rng.integers(0, 300)),
                                  clone_id="AB"[i % 2], copy=float(rng.uniform(1, 4))))
-    df = pd.DataFrame(rows).sample(frac=1.0, random_state=seed).reset_index(drop=True)
+    df = pd.DataFrame(rows)
+    if order == "shuffled":
+        df = df.sample(frac=1.0, random_state=seed).reset_index(drop=True)
+    else:
+        # grouped by cell like concatenated per-cell HMMcopy tables, cells in a random order;
+        # 'cells_split': one cell's block cut in two and moved apart (leaves the block path);
+        # 'cells_unsorted': EVERY cell's loci in one shuffled order (the block path)
+        blocks = [b for _, b in df.groupby("cell_id", sort=False)]
+        perm = np.random.default_rng(seed).permutation(len(blocks))
+        blocks = [blocks[i] for i in perm]
+        if order == "cells_split":
+            b = blocks.pop(0)
+            blocks = [b.iloc[:5]] + blocks + [b.iloc[5:]]
+        elif order == "cells_unsorted":
+            q = np.random.default_rng(seed + 1).permutation(len(blocks[0]))
+            blocks = [b.iloc[q] for b in blocks]
+        df = pd.concat(blocks).reset_index(drop=True)
     if nan_locus:                   # one locus missing in one cell: dropped for every cell
         c0 = df.cell_id.iloc[0]
         df.loc[(df.cell_id == c0) & (df.chr == "2") & (df.start == 1), "reads"] = np.nan
@@ -53,15 +70,24 @@ def _ref_process(cn_s, cn_g1):
                 ids=ids, gc=gam["gc"].to_numpy(np.float32))
 
 
+@pytest.mark.parametrize("order", ["shuffled", "cells", "cells_split", "cells_unsorted"])
 @pytest.mark.parametrize("nan_locus", [False, True])
-def test_process_input_data_matches_pandas(nan_locus):
-    s = _table(9, "s", seed=1, nan_locus=nan_locus)
-    g = _table(6, "g", seed=2, n_libs=3, nan_locus=nan_locus)
+def test_process_input_data_matches_pandas(nan_locus, order):
+    s = _table(9, "s", seed=1, nan_locus=nan_locus, order=order)
+    g = _table(6, "g", seed=2, n_libs=3, nan_locus=nan_locus, order=order)
     ref = _ref_process(s, g)
-    cn_s, cn_g1, inp = prep.process_input_data(s, g)
-    # sorted long tables: same rows in the same order
-    assert (cn_s.index.to_numpy() == ref["cn_s"].index.to_numpy()).all()
-    assert (cn_g1.index.to_numpy() == ref["cn_g1"].index.to_numpy()).all()
+    blocks = []
+    real = prep._cell_blocks
+    prep._cell_blocks = lambda *a: blocks.append(real(*a)) or blocks[-1]
+    try:
+        cn_s, cn_g1, inp = prep.process_input_data(s, g)
+    finally:
+        prep._cell_blocks = real
+    # the per-cell block permutation ran where the table is made of whole per-cell blocks
+    assert [b is not None for b in blocks] == [order in ("cells", "cells_unsorted")] * 2
+    # sorted long tables: same rows in the same order, same columns and dtypes
+    pd.testing.assert_frame_equal(cn_s, ref["cn_s"])
+    pd.testing.assert_frame_equal(cn_g1, ref["cn_g1"])
     np.testing.assert_array_equal(inp.cells_s, ref["s_r"].columns.to_numpy())
     np.testing.assert_array_equal(inp.cells_g, ref["g_r"].columns.to_numpy())
     np.testing.assert_array_equal(inp.loci_chr.astype(str), ref["s_r"].index.get_level_values(0).astype(str))

@@ -262,6 +262,9 @@ def main():
     dt = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in shard.pass_events]))
     shard.pass_events = None
+    # after the timed region: the same shard's HBM streams with no arithmetic (the pattern's
+    # ceiling on this device, this lease) -- pert_stream_ceiling leaves the state unchanged
+    ceil_ms = shard.stream_ceiling_ms() if args.fit != "step1" else None
     t = torch.tensor([dt, kern_ms], dtype=torch.float64, device=device)
     if pg is not None:
         pg.all_reduce(t, op=pg.ReduceOp.MAX)
@@ -307,6 +310,12 @@ def main():
                          "valu_issue_frac": (valu or {}).get("issue_frac")},
             "loss_first": losses[0], "loss_last": losses[-1],
         }
+        if ceil_ms is not None:
+            rec["roofline"]["pattern_ceiling"] = {
+                "ms": ceil_ms, "GB/s": bpc * local_cb / (ceil_ms * 1e-3) / 1e9,
+                "kernel_frac_of_ceiling": ceil_ms / kern_ms,
+                "what": "pert_stream_ceiling: the pass's HBM streams (x, eta code, z/m/v read + written) with no "
+                        "arithmetic, same tiles, same shard, same process"}
         if args.fit == "step2" and args.variant == 3 and shard.fused:
             rec["roofline"]["note"] = ("one launch per step (pert_enum_step): the pass with the reductions and "
                                        "Adam folded in; kernel_ms is that launch")

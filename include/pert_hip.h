@@ -199,6 +199,12 @@ int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream);
 int pert_adam(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
               hipStream_t stream);
 
+/* Diagnostic (bench.py): the HBM streams of pert_enum_pass(PERT_MODE_STEP) -- x, eta code,
+ * z/m/v read and written back unchanged, same grid and tile length -- with no arithmetic.
+ * Its duration is the access pattern's HBM ceiling on the running device; the state is
+ * left bit-identical.  Steps 2/3 shards only. */
+int pert_stream_ceiling(const pert_problem* prob, pert_state* st, hipStream_t stream);
+
 /* Test-only entry points: the per-(bin, cell) arithmetic of pert_math.h evaluated on
  * the host (no GPU needed) or on the device, for the parity suite.  Not used by any
  * product path. */

@@ -26,7 +26,7 @@ BLOCK = 256
 # every symbol include/pert_hip.h declares
 EXPORTED_SYMBOLS = (
     "pert_make_layout", "pert_workspace_sizes", "pert_auto_bins_per_tile", "pert_enum_pass", "pert_obs_pass",
-    "pert_finalize", "pert_adam", "pert_enum_step", "pert_adam_shared", "pert_selftest_nb_lgdiff_host",
+    "pert_finalize", "pert_adam", "pert_enum_step", "pert_adam_shared", "pert_stream_ceiling", "pert_selftest_nb_lgdiff_host",
     "pert_selftest_nb_lgdiff_device", "pert_selftest_enum_cellbin_host", "pert_version",
 )
 
@@ -134,6 +134,7 @@ def load(path: str):
                                       c_void_p]
     handle.pert_adam_shared.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams),
                                         c_void_p]
+    handle.pert_stream_ceiling.argtypes = [POINTER(PertProblem), POINTER(PertState), c_void_p]
     handle.pert_selftest_nb_lgdiff_host.argtypes = [i64, fp, fp, fp, fp]
     handle.pert_selftest_nb_lgdiff_device.argtypes = [i64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     handle.pert_selftest_enum_cellbin_host.argtypes = [i32, i64, fp, fp, fp, fp, c_float, fp, fp, fp, fp,

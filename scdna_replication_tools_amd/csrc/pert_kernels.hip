@@ -1908,6 +1908,55 @@ __global__ void __launch_bounds__(kBlock) adam_kernel(pert_problem pr, pert_stat
   st.adam_v[i] = vv;
 }
 
+// Pattern ceiling (diagnostic): the STEP pass's HBM streams with no arithmetic -- per 64-cell
+// wave tile and bin, x and the eta code read, the P planes of z, m, v read and written back
+// unchanged (the values pass through an opaque register move, so the stores are not folded
+// away and the state is bit-identical afterwards).  Same grid and tile length as the pass:
+// its time is what this access pattern costs in HBM on the box it runs on.
+template <int P>
+__global__ void __launch_bounds__(64) stream_ceiling_kernel(pert_problem pr, pert_state st) {
+  const int lane = threadIdx.x, wt = blockIdx.x, ldn = pr.ldn;
+  const int LT = st.bins_per_tile;
+  const int l0 = blockIdx.y * LT, l1 = min(pr.L, l0 + LT);
+  const size_t t0 = (size_t)wt * pr.L * P * 64 + lane;
+  float zr[P], mr[P], vr[P];
+  float xr = 0.0f;
+  uint32_t cr = 0;
+  auto load = [&](int l) {
+    const size_t o = t0 + (size_t)l * P * 64;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      zr[k] = __builtin_nontemporal_load(st.z_pi + o + k * 64);
+      mr[k] = __builtin_nontemporal_load(st.m_pi + o + k * 64);
+      vr[k] = __builtin_nontemporal_load(st.v_pi + o + k * 64);
+    }
+    xr = pr.reads[(size_t)l * ldn + wt * 64 + lane];
+    cr = pr.eta_code[(size_t)l * ldn + wt * 64 + lane];
+  };
+  float acc = 0.0f;
+  load(l0);
+  for (int l = l0; l < l1; ++l) {
+    float zc[P], mc[P], vc[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      zc[k] = zr[k];
+      mc[k] = mr[k];
+      vc[k] = vr[k];
+    }
+    acc += xr + (float)cr;
+    if (l + 1 < l1) load(l + 1);
+    const size_t o = t0 + (size_t)l * P * 64;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      asm volatile("" : "+v"(zc[k]), "+v"(mc[k]), "+v"(vc[k]));
+      __builtin_nontemporal_store(zc[k], st.z_pi + o + k * 64);
+      __builtin_nontemporal_store(mc[k], st.m_pi + o + k * 64);
+      __builtin_nontemporal_store(vc[k], st.v_pi + o + k * 64);
+    }
+  }
+  asm volatile("" ::"v"(acc));
+}
+
 // Device self-test of nb_lgdiff (accuracy of the special functions on gfx950).
 __global__ void nb_selftest_kernel(int64_t n, const float* d, const float* x, float* lam, float* psi) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2184,6 +2233,23 @@ int pert_adam(const pert_problem* prob, pert_state* st, const pert_adam_hparams*
   const int n = st->lay.n_params;
   hipLaunchKernelGGL(adam_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, *prob, *st, *hp, n);
   return hip_status(hipGetLastError());
+}
+
+int pert_stream_ceiling(const pert_problem* prob, pert_state* st, hipStream_t stream) {
+  if (!problem_ok(prob) || !st || !st->z_pi || !st->m_pi || !st->v_pi || !prob->eta_code) return PERT_E_ARG;
+  if (prob->kind != PERT_KIND_STEP2 && prob->kind != PERT_KIND_STEP3) return PERT_E_ARG;
+  pert_state s2 = *st;
+  s2.bins_per_tile = tile_bins(st);
+  const dim3 grid(enum_cell_tiles(prob, st), (prob->L + s2.bins_per_tile - 1) / s2.bins_per_tile);
+  switch (prob->P) {
+#define PERT_CASE(PP)                                                                          \
+  case PP:                                                                                     \
+    hipLaunchKernelGGL(stream_ceiling_kernel<PP>, grid, dim3(64), 0, stream, *prob, s2);     \
+    return hip_status(hipGetLastError());
+    PERT_ALL_P_CASES
+#undef PERT_CASE
+    default: return PERT_E_UNSUPPORTED_P;
+  }
 }
 
 int pert_selftest_nb_lgdiff_host(int64_t n, const float* d, const float* x, float* lam, float* psi) {

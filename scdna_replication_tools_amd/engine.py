@@ -494,6 +494,26 @@ class PertShard:
                 nat.check(self.lib.pert_enum_pass(ctypes.byref(self._prob), ctypes.byref(self._state),
                                                   ctypes.byref(self._hp), mode, s), "pert_enum_pass")
 
+    def stream_ceiling_ms(self, reps: int = 10) -> float:
+        """Mean duration (HIP events, current stream) of pert_stream_ceiling: the STEP pass's
+        HBM streams with no arithmetic, on this shard's own buffers and tile grid (the state
+        is unchanged).  The pass's time over this one is its fraction of the pattern's
+        ceiling on the running device."""
+        assert self.kind != nat.KIND_STEP1 and self.z_pi is not None
+        s = self._stream()
+        with self._dev():
+            nat.check(self.lib.pert_stream_ceiling(ctypes.byref(self._prob), ctypes.byref(self._state), s),
+                      "pert_stream_ceiling")
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                nat.check(self.lib.pert_stream_ceiling(ctypes.byref(self._prob), ctypes.byref(self._state), s),
+                          "pert_stream_ceiling")
+            e1.record()
+            e1.synchronize()
+        return e0.elapsed_time(e1) / reps
+
     def _finalize(self):
         """Reductions of the pass partials; with a process group, the shard's shared block is
         written to ``grad_local`` and the all-reduce runs on a fresh copy of it, so the sum is

@@ -387,10 +387,24 @@ def process_input_data(cn_s: pd.DataFrame, cn_g1: pd.DataFrame, input_col="reads
 
 
 # --------------------------------------------------------------------------- clones
+def _factorize_sorted_numbers(values):
+    """pd.factorize(values, sort=True) for a numeric column; small non-negative integers
+    (CN states) by one bincount instead of hashing every row."""
+    v = np.asarray(values)
+    if v.size and v.dtype.kind in "iuf":
+        lo, hi = v.min(), v.max()                       # NaN propagates: no fast path
+        if lo >= 0 and hi < 4096 and (v.dtype.kind in "iu" or (v == np.floor(v)).all()):
+            vi = v.astype(np.int64)
+            present = np.bincount(vi, minlength=int(hi) + 1) > 0
+            remap = np.cumsum(present) - 1
+            return remap[vi], np.flatnonzero(present).astype(v.dtype)
+    return pd.factorize(v, sort=True)
+
+
 def _cell_mode(cell_code: np.ndarray, n_cells: int, states: np.ndarray) -> np.ndarray:
     """Per-cell mode of ``states`` (ties to the smallest value, scipy.stats.mode), by
     counting (cell, state) codes."""
-    sc, su = pd.factorize(states, sort=True)
+    sc, su = _factorize_sorted_numbers(states)
     ok = (sc >= 0) & (cell_code >= 0)
     cnt = np.bincount(cell_code[ok] * len(su) + sc[ok], minlength=n_cells * len(su)).reshape(n_cells, len(su))
     return np.asarray(su)[cnt.argmax(axis=1)] if len(su) else np.full(n_cells, np.nan)
@@ -417,8 +431,10 @@ def _majority_ploidy_rows(cn: pd.DataFrame, clone_col="clone_id", cell_col="cell
         n_clones = len(ku)
     cc, kc = cell_code, clone_code
     pl_cell = _cell_mode(cc, n_cells, cn[cn_state_col].to_numpy())
-    pl = pl_cell[np.where(cc >= 0, cc, 0)]
-    pc, pu = pd.factorize(pl, sort=True)
+    # ploidy codes per cell, then per row (the per-cell uniques may include ploidies of cells
+    # without rows here: they only add zero-count columns, which no argmax below picks)
+    pcc, pu = pd.factorize(pl_cell, sort=True)
+    pc = pcc[np.where(cc >= 0, cc, 0)]
     ok = (kc >= 0) & (pc >= 0) & (cc >= 0)
     cnt = np.bincount(kc[ok] * len(pu) + pc[ok], minlength=n_clones * len(pu)).reshape(n_clones, len(pu))
     keep_pc = cnt.argmax(axis=1)
@@ -498,19 +514,30 @@ def consensus_clone_profiles(cn: pd.DataFrame, col_name: str, clone_col="clone_i
             cc, cells = _sorted_codes(cn[cell_col].to_numpy())
         cc = np.where(rows, cc, -1)
         rows &= _majority_ploidy_rows(cn, clone_col, cell_col, cn_state_col, cc, len(cells), kc, len(ku))
-    hc, hu = _factorize(cn[chr_col].to_numpy())
-    st = cn[start_col].to_numpy()
-    ok = hc >= 0
-    lc, lu = pd.factorize(np.where(ok, hc.astype(np.int64) * (1 << 40) + np.where(ok, st, 0).astype(np.int64), -1))
+    if keys is not None and len(keys.cell_code) == len(cn) and isinstance(cn[chr_col].dtype, pd.CategoricalDtype):
+        # the sorted table's locus codes (sorted (chr category, start) uniques), no re-hashing
+        lc = keys.locus_code
+        ok = lc >= 0
+        n_loci = keys.loci_start.size
+        chr_lab, start_lab = keys.loci_chr, keys.loci_start
+        valid_l = np.ones(n_loci, bool)
+    else:
+        hc, hu = _factorize(cn[chr_col].to_numpy())
+        st = cn[start_col].to_numpy()
+        ok = hc >= 0
+        lc, lu = pd.factorize(np.where(ok, hc.astype(np.int64) * (1 << 40) + np.where(ok, st, 0).astype(np.int64), -1))
+        n_loci = len(lu)
+        hu_arr = np.asarray(hu, dtype=object)
+        chr_lab = hu_arr[(lu >> 40).astype(np.int64) % max(len(hu_arr), 1)]
+        start_lab = lu & ((1 << 40) - 1)
+        valid_l = np.asarray(lu) >= 0
     grp = np.where(rows & ok, lc * len(ku) + kc, -1)
-    med = _group_median(grp, cn[col_name].to_numpy(np.float64), len(lu) * len(ku))
-    hu_arr = np.asarray(hu, dtype=object)
-    chr_lab = hu_arr[(lu >> 40).astype(np.int64) % max(len(hu_arr), 1)]
+    med = _group_median(grp, cn[col_name].to_numpy(np.float64), n_loci * len(ku))
     if isinstance(cn[chr_col].dtype, pd.CategoricalDtype):
         chr_lab = pd.Categorical(chr_lab, categories=cn[chr_col].cat.categories, ordered=cn[chr_col].cat.ordered)
-    idx = pd.MultiIndex.from_arrays([chr_lab, lu & ((1 << 40) - 1)], names=[chr_col, start_col])
-    prof = pd.DataFrame(med.reshape(len(lu), len(ku)), index=idx, columns=pd.Index(ku, name=clone_col))
-    prof = prof[np.asarray(lu) >= 0].dropna(how="all").dropna(axis=1, how="all")
+    idx = pd.MultiIndex.from_arrays([chr_lab, start_lab], names=[chr_col, start_col])
+    prof = pd.DataFrame(med.reshape(n_loci, len(ku)), index=idx, columns=pd.Index(ku, name=clone_col))
+    prof = prof[valid_l].dropna(how="all").dropna(axis=1, how="all")
     return prof.sort_index()
 
 

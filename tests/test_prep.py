@@ -113,11 +113,19 @@ def test_pivot_averages_duplicates_and_drops_nan_keys():
     np.testing.assert_array_equal(p.values, [[3.0, 1.0], [np.nan, 5.0]])
 
 
-def test_consensus_clone_profiles_matches_pandas():
+@pytest.mark.parametrize("col,with_keys", [("copy", False), ("state", False), ("copy", True), ("state", True)])
+def test_consensus_clone_profiles_matches_pandas(col, with_keys):
+    """Float values (median by sort) and integer states (median by histogram); on the raw
+    table, or on the sorted table with its integer keys (the run_pert_model path)."""
     from scipy.stats import mode
     g = _table(10, "g", seed=3)
     g.loc[g.cell_id == g.cell_id.iloc[0], "state"] = 7            # an off-ploidy cell
-    got = prep.consensus_clone_profiles(g, "copy")
+    g.loc[g.cell_id == g.cell_id.iloc[1], "state"] = 3            # an even state count: half-way medians
+    if with_keys:
+        gs, keys = prep._sorted_table(g, "cell_id", "chr", "start")
+        got = prep.consensus_clone_profiles(gs, col, keys=keys)
+    else:
+        got = prep.consensus_clone_profiles(g, col)
     # compute_consensus_clone_profiles.py:42-88 restated
     cn = g[g["clone_id"] != "None"].copy()
     pl = {c: mode(grp["state"], keepdims=False)[0] for c, grp in cn.groupby("cell_id")}
@@ -127,7 +135,7 @@ def test_consensus_clone_profiles_matches_pandas():
         keep = grp.groupby("ploidy").size().idxmax()
         pieces.append(grp[grp["ploidy"] == keep])
     cn = pd.concat(pieces, ignore_index=True)
-    ref = cn.pivot_table(index=["chr", "start"], columns="clone_id", values="copy", aggfunc="median")
+    ref = cn.pivot_table(index=["chr", "start"], columns="clone_id", values=col, aggfunc="median")
     ref.index = pd.MultiIndex.from_arrays([ref.index.get_level_values(0).astype(str), ref.index.get_level_values(1)])
     got.index = pd.MultiIndex.from_arrays([got.index.get_level_values(0).astype(str), got.index.get_level_values(1)])
     got = got.loc[ref.index, ref.columns]

@@ -164,8 +164,10 @@ def main():
     ap.add_argument("--bins-per-tile", type=int, default=0)
     ap.add_argument("--fit", default="step2", choices=["step1", "step2", "step3"],
                     help="which SVI fit's step to time (the metric is step 2's)")
-    ap.add_argument("--variant", type=int, default=0, help="enumerated-pass kernel: 0 LDS-DMA, 1 register, 3 three-wave streamed")
-    ap.add_argument("--no-fused", action="store_true", help="variant 3: separate finalize / adam launches")
+    ap.add_argument("--variant", type=int, default=3, help="enumerated-pass kernel: 3 three-wave streamed (default), "
+                    "0 two-wave LDS-DMA, 1 register pipeline")
+    ap.add_argument("--fused", action="store_true", help="variant 3: one launch per step (pert_enum_step)")
+    ap.add_argument("--no-fused", action="store_true", help="(the default) separate finalize / adam launches")
     ap.add_argument("--cells", type=int, default=0, help="override the config's cell count (per job)")
     ap.add_argument("--subdivide", type=int, default=0, help="override the config's bin subdivision")
     ap.add_argument("--reads-per-cell", type=float, default=1e6, help="synthetic library size per cell")
@@ -220,7 +222,7 @@ def main():
     allreduce = make_allreduce()
     libs = np.zeros(n1 - n0, int)
     common = dict(device=device, is_root=(rank == 0), allreduce=allreduce, bins_per_tile=args.bins_per_tile,
-                  variant=args.variant, fused=not args.no_fused)
+                  variant=args.variant, fused=args.fused and not args.no_fused)
     if args.fit == "step1":
         # step 1 (pert_model.py:718-774): the same cells as G1/2 cells, doubled with rep 0 / 1
         st2 = np.concatenate([states, states], 1)
@@ -284,7 +286,8 @@ def main():
         if os.path.exists(args.pmc) and args.fit == "step2":
             try:
                 pm = json.load(open(args.pmc))
-                if pm.get("config") == args.config and int(pm.get("cells", -1)) == n1 - n0:
+                if (pm.get("config") == args.config and int(pm.get("cells", -1)) == n1 - n0
+                        and pm.get("kernel") == kname):
                     traffic = pm.get("hbm_bytes_per_launch")
                     valu = pm.get("valu")
             except (OSError, ValueError):

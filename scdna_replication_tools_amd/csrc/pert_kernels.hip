@@ -29,6 +29,7 @@ constexpr int kBlock = PERT_BLOCK;
 constexpr int kWaves = kBlock / 64;
 constexpr int kDefaultLT = 32;
 constexpr int kMaxLT = 64;
+constexpr int kShortLT3 = 12;                    // variant 3's tile length on multi-round launches
 constexpr int kEtaLdsFloats = 1024;   // eta tables up to 4 KB are staged in LDS
 constexpr int kBlkSlots = 4;      // loss, d/da, sum delta, sum gdd (step 1)
 constexpr float kHalfLog2PiF = 0.918938533204672742f;
@@ -2137,6 +2138,26 @@ int pert_auto_bins_per_tile(const pert_problem* prob, int32_t variant, int32_t* 
   // cells this takes two rounds of 27 bins over one of 54 (-3 % kernel, tools/lt_sweep.sh).
   constexpr int kTilePrologue = 2;
   const long n_ct = (prob->N + 63) / 64;
+  if (variant == 3) {
+    // The three-wave pass streams at 0.95-0.99 of its own HBM pattern ceiling with short
+    // tiles whenever the launch runs several rounds (12 bins: 2,500-10,000 cells; the
+    // cell-tile x bin-tile sweep of profiles/r02q, r02r).  A shard small enough that ONE
+    // round of longer tiles leaves some slots free (1,250 cells, the per-rank shard of an
+    // 8-GPU run) does better that way (0.87 vs 0.86 at 12 bins): each wave pays one tile
+    // prologue and the round has no tail of late tiles.  Take the shortest such tile
+    // from 36 bins up, else 12.
+    const int occ = step_occupancy(*prob, kShortLT3, 3);
+    const long slots = (long)ncu * (occ > 0 ? occ : 8);
+    for (int lt = 36; lt <= kMaxLT; ++lt) {
+      const long tiles = n_ct * ((prob->L + lt - 1) / lt);
+      if (20 * tiles <= 17 * slots) {
+        *out = lt;
+        return PERT_OK;
+      }
+    }
+    *out = kShortLT3;
+    return PERT_OK;
+  }
   long best = -1;
   int best_lt = kDefaultLT;
   for (int lt = kMaxLT; lt >= 8; --lt) {

@@ -227,7 +227,7 @@ class PertShard:
                  pi_init=None, device=None, lr: float = 0.05, betas=ADAM_BETAS, eps: float = ADAM_EPS,
                  is_root: bool = True, n_cells_total: Optional[int] = None,
                  allreduce: Optional[Callable[[torch.Tensor], None]] = None,
-                 dirichlet_mode: str = "torch32", bins_per_tile: int = 0, variant: int = 0, fused: bool = True,
+                 dirichlet_mode: str = "torch32", bins_per_tile: int = 0, variant: int = 3, fused: bool = False,
                  lib=None):
         self.lib = nat.lib() if lib is None else lib        # another build of the ABI (A/B tools)
         self.kind = int(kind)

@@ -154,6 +154,44 @@ def profile_numbers(prof_dir: str, kernel: str):
             "pmc": ent.get("pmc", {})}
 
 
+def fullfit_c1():
+    """configs[0] stand-in (400 S + 400 G1/2 cells x 271 bins, diploid; tests/_configs.py) under
+    inference_tutorial.ipynb cell 9's call: the product's full three-step fit on the GPU
+    (scRT(...).infer(level='pyro'), host prep included) and, as the measured CPU baseline, the
+    same chained fit on the oracle (tests/_chain.py: the torch-CPU tensor algebra Pyro runs,
+    on every CPU of the process's share) from the same prep -- both timed end to end, not
+    extrapolated.  One JSON line."""
+    import contextlib
+    import io
+    from tests._chain import oracle_chain
+    from tests._configs import c1_tables, tutorial_scrt
+    s, g, truth = c1_tables()
+    torch.zeros(1, device="cuda")
+    with contextlib.redirect_stdout(io.StringIO()):
+        t0 = time.perf_counter()
+        sc = tutorial_scrt(s.copy(), g.copy())
+        cn_s_out, supp_s, cn_g1_out, supp_g1 = sc.infer(level='pyro')
+        torch.cuda.synchronize()
+        t_gpu = time.perf_counter() - t0
+    m = sc.model
+    share = cpu_share()
+    torch.set_num_threads(share["cores"])
+    m2 = tutorial_scrt(s.copy(), g.copy(), device="cpu")._pert_model()
+    t0 = time.perf_counter()
+    res = oracle_chain(m2, torch.float32)
+    t_cpu = time.perf_counter() - t0
+    iters = {k: len(res[v]) for k, v in (("step1", "losses_g"), ("step2", "losses_s"), ("step3", "losses_s2"))}
+    mm = cn_s_out.merge(truth, on=["cell_id", "chr", "start"])
+    rec = {"metric": "full 3-step PERT fit wall-clock, configs[0] stand-in (400+400 cells x 271 bins, max_iter 200)",
+           "gpu_s": t_gpu, "gpu_timings_s": m.timings, "gpu_iters": m.iters,
+           "cpu_baseline": {"seconds": t_cpu, "iters": iters, "cores": share["cores"], "cpu_model": share["cpu_model"],
+                            "kind": "port", "what": "oracle chain (tests/_chain.py), fp32, measured end to end"},
+           "speedup": t_cpu / t_gpu, "unit": "s", "higher_is_better": False,
+           "acc_cn_vs_truth": float((mm["model_cn_state"] == mm["true_somatic_cn"]).mean()),
+           "acc_rep_vs_truth": float((mm["model_rep_state"] == mm["true_rep"]).mean())}
+    print(json.dumps(rec), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -177,7 +215,12 @@ def main():
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--profile", default="", help="tools/profile.sh output dir of this command: report the "
                     "roofline fraction recomputed from its kernel trace and its PMC HBM bytes")
+    ap.add_argument("--fullfit-c1", action="store_true",
+                    help="time the configs[0] stand-in's full fit on the GPU and on the CPU oracle, then exit")
     args = ap.parse_args()
+    if args.fullfit_c1:
+        fullfit_c1()
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -1130,6 +1130,9 @@ __global__ void __launch_bounds__(kBlock) obs_kernel(pert_problem pr, pert_state
 // (step 1) each workgroup's ELBO / d/da / lambda sums (summed by the last block).
 constexpr int kFinBlock = 1024;
 constexpr int kFinG = kFinBlock / 64;
+#ifndef PERT_FIN_U
+#define PERT_FIN_U 4
+#endif
 __host__ __device__ constexpr int fin_slots(int n_libs, int K1) { return 2 * n_libs * K1 + 2; }
 
 // ---- per-bin: d(-ELBO)/dz_rho   (rho ~ Beta(1,1) has zero log density, :574)
@@ -1249,7 +1252,7 @@ template <int K1T>
 __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_state& st, int cb, int n_bt,
                                           bool stopped, double (*s_g)[64]) {
   constexpr int kCS = K1T + 1;
-  constexpr int kFinU = K1T <= 5 ? 4 : 1;       // bin tiles in flight per thread
+  constexpr int kFinU = K1T <= 5 ? PERT_FIN_U : 1;   // bin tiles in flight per thread
   const int tid = threadIdx.x, lane = tid & 63, grp = tid >> 6;
   const int N = pr.N, K1 = (K1T == PERT_MAX_K1) ? pr.K1 : K1T, nl = pr.n_libs;
   const pert_layout lay = st.lay;

@@ -109,3 +109,30 @@ def test_scrt_polyclonal_without_clone_labels():
     acc_cn = (ok["model_cn_state"] == ok["true_somatic_cn"]).mean()
     acc_rep = (cn_s_out["model_rep_state"] == cn_s_out["true_rep"]).mean()
     assert acc_cn > 0.97 and acc_rep > 0.85, (acc_cn, acc_rep)
+
+
+def test_scrt_polyclonal_full_genome():
+    """configs[1] stand-in at the configs' genome size: polyclonal sample without clone labels
+    on the full 5,451-bin 500 kb grid (600 + 600 cells, three clones) through
+    scRT(clone_col=None).infer('pert'): KMeans + BIC clustering, S-cell assignment and the three
+    fits; clusters must be the simulated clones and the calls must recover the truth."""
+    import pandas as pd
+    from scdna_replication_tools_amd.infer_scRT import scRT
+    from scdna_replication_tools_amd.simulator import simulate, to_long_form
+    sim = simulate(n_s=600, n_g=600, num_reads=1e6, seed=11)
+    df_s, df_g = to_long_form(sim, n_libs=1, copy_from="reads")
+    truth_g = df_g.drop_duplicates("cell_id").set_index("cell_id")["clone_id"]
+    m = scRT(df_s.drop(columns=["clone_id"]), df_g.drop(columns=["clone_id"]), clone_col=None,
+             cn_prior_method='g1_clones', max_iter=400, min_iter=50)
+    cn_s_out, supp_s, cn_g1_out, supp_g1 = m.infer(level='pert')
+    cl = m.clusters.set_index("cell_id")["cluster_id"]
+    t = pd.crosstab(cl.to_numpy(), truth_g.loc[cl.index].to_numpy())
+    assert t.shape == (3, 3) and ((t > 0).sum(1) == 1).all() and ((t > 0).sum(0) == 1).all()
+    to_clone = t.idxmax(axis=1)
+    right = cn_s_out["cluster_id"].map(to_clone) == cn_s_out["cell_id"].map(
+        df_s.drop_duplicates("cell_id").set_index("cell_id")["clone_id"])
+    assert right.mean() > 0.95
+    acc_cn = (cn_s_out["model_cn_state"] == cn_s_out["true_somatic_cn"]).mean()
+    acc_rep = (cn_s_out["model_rep_state"] == cn_s_out["true_rep"]).mean()
+    print("polyclonal full genome: cn {:.5f} rep {:.5f} timings {}".format(acc_cn, acc_rep, m.model.timings))
+    assert acc_cn > 0.99 and acc_rep > 0.98, (acc_cn, acc_rep)

@@ -30,6 +30,7 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kDefaultLT = 32;
 constexpr int kMaxLT = 64;
 constexpr int kShortLT3 = 12;                    // variant 3's tile length on multi-round launches
+constexpr int kLongLT3 = 18;                     // ... and on launches of 8 rounds or more
 constexpr int kEtaLdsFloats = 1024;   // eta tables up to 4 KB are staged in LDS
 constexpr int kBlkSlots = 4;      // loss, d/da, sum delta, sum gdd (step 1)
 constexpr float kHalfLog2PiF = 0.918938533204672742f;
@@ -2158,7 +2159,10 @@ int pert_auto_bins_per_tile(const pert_problem* prob, int32_t variant, int32_t* 
         return PERT_OK;
       }
     }
-    *out = kShortLT3;
+    // many rounds (10 k cells: 15 rounds at 18 bins) -> 18 bins: the same kernel as 12 and a
+    // third fewer per-cell partials for finalize (step -1 %, profiles/r02u); fewer -> 12
+    const long tiles18 = n_ct * ((prob->L + kLongLT3 - 1) / kLongLT3);
+    *out = tiles18 >= 8 * slots ? kLongLT3 : kShortLT3;
     return PERT_OK;
   }
   long best = -1;

@@ -41,7 +41,7 @@ from ._native import KIND_STEP1, KIND_STEP2, KIND_STEP3
 from .engine import EtaCodebook, PertShard
 from .init import init_params
 from .sharding import cell_bounds, make_allreduce
-from .tau_init import guess_times_batched
+from .tau_init import guess_times_batched, prewarm_pool
 
 log = logging.getLogger("scdna_replication_tools_amd.pert_model")
 
@@ -374,6 +374,8 @@ class pert_infer_scRT():
         dd = _Dist(self._group)
         if self.device.type == "cuda" and self.device.index is not None:
             torch.cuda.set_device(self.device)
+        if self.tau_init_method != 'sklearn':
+            prewarm_pool(self.n_jobs if self.n_jobs != 1 else -1)   # overlaps prep and step 1
         tic = time.perf_counter()
         inp = self._prepare()
         n_libs = self.L

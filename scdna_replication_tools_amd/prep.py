@@ -107,19 +107,39 @@ def _cell_blocks(cck: np.ndarray, lkey: np.ndarray):
     return (bp[:, None] * L + q[None, :]).reshape(-1)
 
 
-def _take_columns(df: pd.DataFrame, order: np.ndarray) -> pd.DataFrame:
-    """``df.take(order)`` built column by column with ``np.take`` (pandas' take goes through
-    its generic take_nd, 2-3x slower on object columns); extension columns use their own take."""
+def _take_columns(df: pd.DataFrame, order: np.ndarray, codes: Optional[dict] = None,
+                  replace: Optional[dict] = None) -> pd.DataFrame:
+    """``df.take(order)`` built column by column: numeric columns by ``np.take`` on a few
+    threads (it releases the GIL), object (label) columns as ``uniques[codes[order]]`` from
+    their factorisation where it is known (``codes``: (codes, uniques) by column name) -- a
+    gather from a small array whose objects are shared, instead of touching one object per
+    row -- and
+    ``replace``: columns given directly (already in the new order)."""
     from concurrent.futures import ThreadPoolExecutor
+    codes = codes or {}
+    replace = replace or {}
+    names = list(df.columns)
     sers = [df.iloc[:, j] for j in range(df.shape[1])]
-    num = [j for j, ser in enumerate(sers) if isinstance(ser.dtype, np.dtype) and ser.dtype != object]
     cols = [None] * len(sers)
-    # numeric gathers release the GIL: run them on a few threads beside the object ones
-    with ThreadPoolExecutor(max_workers=min(8, max(1, len(num)))) as ex:
-        futs = {j: ex.submit(np.take, sers[j].to_numpy(), order) for j in num}
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        futs = {}
         for j, ser in enumerate(sers):
-            if j not in futs:
-                cols[j] = np.take(ser.to_numpy(), order) if isinstance(ser.dtype, np.dtype) else ser.take(order).array
+            name = names[j]
+            if name in replace:
+                cols[j] = replace[name]
+            elif isinstance(ser.dtype, np.dtype) and ser.dtype != object:
+                futs[j] = ex.submit(np.take, ser.to_numpy(), order)
+            elif ser.dtype == object:
+                cu = codes.get(name)
+                if cu is None or len(cu[1]) * 8 > len(order):   # no codes / mostly distinct labels
+                    cols[j] = np.take(ser.to_numpy(), order)
+                else:
+                    uext = np.empty(len(cu[1]) + 1, dtype=object)
+                    uext[:-1] = cu[1]
+                    uext[-1] = np.nan                     # code -1 (a missing label)
+                    futs[j] = ex.submit(lambda c=cu[0], ue=uext: ue[np.take(c, order)])
+            else:
+                cols[j] = ser.take(order).array
         for j, f in futs.items():
             cols[j] = f.result()
     out = pd.DataFrame(dict(enumerate(cols)), index=df.index.take(order), copy=False)
@@ -150,11 +170,13 @@ def _sorted_table(cn: pd.DataFrame, cell_col: str, chr_col: str, start_col: str,
         ok = cn[notna_col].notna().to_numpy()
         if not ok.all():
             order = order[ok[order]]
+    chr_cat = pd.Categorical.from_codes(ch[order], categories=CHR_ORDER)
     if order.size == len(cn) and (order.size == 0 or (order[1:] > order[:-1]).all()):
         out = cn.copy(deep=False)                        # already sorted and complete: no gather
+        out[chr_col] = chr_cat
     else:
-        out = _take_columns(cn, order)
-    out[chr_col] = pd.Categorical.from_codes(ch[order], categories=CHR_ORDER)
+        out = _take_columns(cn, order, codes={cell_col: (cc, np.asarray(cells, dtype=object))},
+                            replace={chr_col: chr_cat})
     return out, TableKeys.from_codes(cc[order], cells, ch[order], st[order])
 
 

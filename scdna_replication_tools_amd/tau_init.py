@@ -291,6 +291,45 @@ def _binarize(Xraw: torch.Tensor, tie_bias: float, with_minor: bool = False):
     return frac, fragile | frag_pp | frag_scan | (minor > 0)
 
 
+def _pool_size(n_jobs: int) -> int:
+    return n_jobs if n_jobs > 0 else min(16, len(os.sched_getaffinity(0)))
+
+
+_WARM = {}
+
+
+def _warm_worker():
+    import sklearn.mixture  # noqa: F401  (the per-cell path's import, done once per worker)
+    return 0
+
+
+def prewarm_pool(n_jobs: int = -1):
+    """Start the joblib (loky) worker processes of the per-cell path in a background thread,
+    so their start-up (a few seconds: interpreter + sklearn import per worker) overlaps the
+    host prep and the first fits instead of delaying guess_times; guess_times_batched waits
+    for it and reuses the same executor."""
+    import threading
+    nj = _pool_size(n_jobs)
+    if nj <= 1 or nj in _WARM:
+        return
+
+    def run():
+        from joblib import Parallel, delayed
+        Parallel(n_jobs=nj)(delayed(_warm_worker)() for _ in range(nj))
+
+    th = threading.Thread(target=run, name="pert-tau-pool", daemon=True)
+    _WARM[nj] = th
+    th.start()
+
+
+def _pool_ready(n_jobs: int) -> bool:
+    th = _WARM.get(_pool_size(n_jobs))
+    if th is None:
+        return False
+    th.join()                              # never two executors being built at once
+    return True
+
+
 def guess_times_batched(reads: np.ndarray, cn_states: np.ndarray, upsilon: float = 6, device=None,
                         n_jobs: int = -1):
     """pert_model.py:426-457: (t_init, t_alpha_prior, t_beta_prior), all cells at once; the
@@ -316,10 +355,10 @@ def guess_times_batched(reads: np.ndarray, cn_states: np.ndarray, upsilon: float
         from .prep import manhattan_binarization
         cols = norm[:, torch.as_tensor(redo, device=dev)].cpu().numpy()
         jobs = [cols[:, j].reshape(-1, 1) for j in range(redo.size)]
-        if redo.size > 64 and n_jobs != 1:
+        warm = _pool_ready(n_jobs)
+        if n_jobs != 1 and (redo.size > 64 or (warm and redo.size > 4)):
             from joblib import Parallel, delayed
-            nj = n_jobs if n_jobs > 0 else min(16, len(os.sched_getaffinity(0)))
-            res = Parallel(n_jobs=nj)(delayed(manhattan_binarization)(c) for c in jobs)
+            res = Parallel(n_jobs=_pool_size(n_jobs))(delayed(manhattan_binarization)(c) for c in jobs)
         else:
             res = [manhattan_binarization(c) for c in jobs]
         for j, n in enumerate(redo):

@@ -139,6 +139,53 @@ def cpu_baseline(data, n_cells: int, steps: int):
             "cgroup_quota_cores": share["cgroup_quota_cores"]}
 
 
+def cpu_extrapolation(sim, iters, n_sample):
+    """The oracle (torch-CPU restatement of the tensor algebra Pyro runs) timed per SVI step
+    on an n_sample-cell slice at full L, scaled linearly in cells and by the GPU run's
+    iteration counts (C3/C4 CPU full fits are extrapolated)."""
+    import torch
+    from oracle import pert_oracle as po
+    threads = cpu_share()["cores"]
+    torch.set_num_threads(threads)
+    L = sim.n_bins
+    P, K = 13, 4
+    n = min(n_sample, sim.reads_s.shape[1])
+    gc = torch.tensor(sim.gc, dtype=torch.float32)
+    # step 2 (and 3: the same model on G1 cells)
+    states = torch.tensor(sim.cn_s[:, :n], dtype=torch.long)
+    etas = torch.ones(L, n, P)
+    etas.scatter_(2, states.unsqueeze(-1), 1e6)
+    bm = torch.zeros(1, K + 1)
+    bm[0, K - 1] = 0.5
+    p2 = po.OracleProblem("step2", torch.tensor(sim.reads_s[:, :n], dtype=torch.float32), gc,
+                          torch.zeros(n, dtype=torch.long), 1, P, K, etas=etas, lamb=torch.tensor([0.75]),
+                          beta_means=bm, t_init=torch.full((n,), 0.5))
+    z2 = po.init_params(p2, seed=0)
+    po.fit(p2, z2, max_iter=1, min_iter=100, cell_chunk=64)
+    t0 = time.perf_counter()
+    po.fit(p2, z2, max_iter=2, min_iter=100, cell_chunk=64)
+    t2 = (time.perf_counter() - t0) / 2 / n                        # s per step per cell
+    # step 1: G1 cells doubled, cn / rep observed
+    g = torch.tensor(sim.reads_g[:, :n], dtype=torch.float32)
+    cg = torch.tensor(sim.cn_g[:, :n], dtype=torch.float32)
+    p1 = po.OracleProblem("step1", torch.cat([g, g], 1), gc, torch.zeros(2 * n, dtype=torch.long), 1, P, K,
+                          cn_obs=torch.cat([cg, cg], 1),
+                          rep_obs=torch.cat([torch.zeros_like(cg), torch.ones_like(cg)], 1))
+    z1 = po.init_params(p1, seed=0)
+    po.fit(p1, z1, max_iter=1, min_iter=100, cell_chunk=128)
+    t0 = time.perf_counter()
+    po.fit(p1, z1, max_iter=2, min_iter=100, cell_chunk=128)
+    t1 = (time.perf_counter() - t0) / 2 / (2 * n)
+    N_s, N_g = sim.reads_s.shape[1], sim.reads_g.shape[1]
+    return {"kind": "port (oracle fp32, extrapolated: per-step time on a {}-cell slice x cells x the GPU run's "
+                    "iteration counts)".format(n),
+            "cores": threads,
+            "step1_s": t1 * 2 * N_g * iters.get("step1", 0),
+            "step2_s": t2 * N_s * iters.get("step2", 0),
+            "step3_s": t2 * N_g * iters.get("step3", 0),
+            "per_step_s": {"step1": t1 * 2 * N_g, "step2": t2 * N_s, "step3": t2 * N_g}}
+
+
 def profile_numbers(prof_dir: str, kernel: str):
     """The dominant kernel's average duration (rocprofv3 kernel trace) and HBM bytes per
     launch (PMC passes) from a tools/profile.sh run of this same command line

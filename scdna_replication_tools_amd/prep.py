@@ -367,12 +367,20 @@ def process_input_data(cn_s: pd.DataFrame, cn_g1: pd.DataFrame, input_col="reads
                        cn_state_col="state"):
     """pert_model.py:133-191 (the unused rt prior aside).  Returns the sorted,
     NaN-filtered long tables and a ``PertInputs``."""
-    cn_g1, kg = _sorted_table(cn_g1, cell_col, chr_col, start_col, notna_col=input_col)
-    cn_s, ks = _sorted_table(cn_s, cell_col, chr_col, start_col, notna_col=input_col)
-    pg_r = drop_incomplete_loci(pivot_cells_by_loci(cn_g1, input_col, cell_col, chr_col, start_col, kg))
-    pg_s = drop_incomplete_loci(pivot_cells_by_loci(cn_g1, cn_state_col, cell_col, chr_col, start_col, kg))
-    ps_r = drop_incomplete_loci(pivot_cells_by_loci(cn_s, input_col, cell_col, chr_col, start_col, ks))
-    ps_s = drop_incomplete_loci(pivot_cells_by_loci(cn_s, cn_state_col, cell_col, chr_col, start_col, ks))
+    from concurrent.futures import ThreadPoolExecutor
+
+    def table(cn):
+        # the two tables are independent: sorted and pivoted on two threads (the numpy
+        # passes release the GIL; the object-column passes interleave)
+        cn, k = _sorted_table(cn, cell_col, chr_col, start_col, notna_col=input_col)
+        r = drop_incomplete_loci(pivot_cells_by_loci(cn, input_col, cell_col, chr_col, start_col, k))
+        st = drop_incomplete_loci(pivot_cells_by_loci(cn, cn_state_col, cell_col, chr_col, start_col, k))
+        return cn, k, r, st
+
+    with ThreadPoolExecutor(max_workers=2) as ex:
+        fg, fs = ex.submit(table, cn_g1), ex.submit(table, cn_s)
+        cn_g1, kg, pg_r, pg_s = fg.result()
+        cn_s, ks, ps_r, ps_s = fs.result()
     assert pg_s.values.shape == pg_r.values.shape                      # :153
     assert ps_r.values.shape[0] == pg_r.values.shape[0]                 # :154
     ps_s = _align(ps_s, ps_r.loci_chr, ps_r.loci_start) if ps_s.values.shape == ps_r.values.shape else ps_s

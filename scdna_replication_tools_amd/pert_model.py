@@ -27,6 +27,7 @@ and ``process_group`` (a torch.distributed group; default: the world when initia
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import os
 import time
@@ -379,11 +380,27 @@ class pert_infer_scRT():
         tic = time.perf_counter()
         inp = self._prepare()
         n_libs = self.L
-        profiles = prep.consensus_clone_profiles(
-            self.cn_g1, self.cn_state_col, clone_col=self.clone_col, cell_col=self.cell_col,
-            chr_col=self.chr_col, start_col=self.start_col, cn_state_col=self.cn_state_col, keys=inp.keys_g)
-        etas = self._build_etas(inp, profiles)
         self.timings["prep"] = time.perf_counter() - tic
+        # host work that only steps 2/3 need runs on a helper thread while step 1 fits on the
+        # device: the consensus profiles and the step-2 prior, then (during step 2) the
+        # step-3 prior and tau initialisation on a side stream
+        from concurrent.futures import ThreadPoolExecutor
+        helper = ThreadPoolExecutor(max_workers=1, thread_name_prefix="pert-prep")
+
+        def on_device(fn, *a):
+            # the HIP runtime's current device is per thread: the helper uses the fit's device
+            if self.device.type != "cuda":
+                return fn(*a)
+            with torch.cuda.device(self.device):
+                return fn(*a)
+
+        def priors():
+            profiles = prep.consensus_clone_profiles(
+                self.cn_g1, self.cn_state_col, clone_col=self.clone_col, cell_col=self.cell_col,
+                chr_col=self.chr_col, start_col=self.start_col, cn_state_col=self.cn_state_col, keys=inp.keys_g)
+            return profiles, self._build_etas(inp, profiles)
+
+        fut_priors = helper.submit(on_device, priors)
 
         # ---- step 1: G1/2 cells doubled, cn / rep observed (:718-774)
         st_g2, rd_g2, lb_g2, rep_g2 = prep.make_g1_g2_training_data(inp.states_g, inp.reads_g, inp.libs_g)
@@ -398,7 +415,12 @@ class pert_infer_scRT():
 
         # ---- step 2: S cells, enumerated (:776-830)
         tic = time.perf_counter()
+        profiles, etas = fut_priors.result()
+        self.timings["prep"] += time.perf_counter() - tic            # the part step 1 did not hide
+        tic = time.perf_counter()
         t_init, _, _ = self._guess_times(inp.reads_s, etas.argmax_states())
+        # (submitted after the step-2 initialiser: the two never share the per-cell pool)
+        fut_prep3 = helper.submit(on_device, self._prep_step3, inp, profiles) if self.run_step3 else None
         self.timings["guess_times_s"] = time.perf_counter() - tic
         ploidy = etas.argmax_states().astype(np.float32).mean(0)
         init2 = init_params(KIND_STEP2, inp.reads_s, inp.libs_s, n_libs, P, K, ploidy=ploidy, t_init=t_init,
@@ -422,10 +444,9 @@ class pert_infer_scRT():
         if self.run_step3:
             # ---- step 3: G1 cells with rho, a frozen (:834-896)
             tic = time.perf_counter()
-            etas2 = self._clone_prior(self.cn_g1, inp.cells_g, profiles, keys=inp.keys_g)
-            t_init2, _, _ = self._guess_times(inp.reads_g, etas2.argmax_states())
+            etas2, t_init2 = fut_prep3.result()
             ploidy2 = etas2.argmax_states().astype(np.float32).mean(0)
-            self.timings["prep_step3"] = time.perf_counter() - tic
+            self.timings["prep_step3"] = time.perf_counter() - tic      # the part step 2 did not hide
             init3 = init_params(KIND_STEP3, inp.reads_g, inp.libs_g, n_libs, P, K, ploidy=ploidy2,
                                 t_init=t_init2, beta_means=beta_means_fit, seed=self.seed, method=self.init_method)
             s3 = self._shard(KIND_STEP3, dd, inp.reads_g, inp.libs_g, init3, eta=etas2, lamb=float(lambda_fit[0]),
@@ -441,8 +462,22 @@ class pert_infer_scRT():
                 self.cn_g1, trace_s2, self._axes(inp.cells_g, inp.keys_g), lambda_fit, losses_g, losses_s2)
             self.timings["decode_package_g"] = time.perf_counter() - tic
             del s3
+        helper.shutdown(wait=True)
         self.timings["total"] = time.perf_counter() - t_all
         return cn_s_out, supp_s_out_df, cn_g1_out, supp_g1_out_df
+
+    def _prep_step3(self, inp, profiles):
+        """Step 3's clone prior on the G1/2 cells and their tau initialisation (:836-858), on
+        the helper thread while step 2 fits: the device part of the initialiser on a side
+        stream of its own."""
+        stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+        with ctx:
+            etas2 = self._clone_prior(self.cn_g1, inp.cells_g, profiles, keys=inp.keys_g)
+            t_init2, _, _ = self._guess_times(inp.reads_g, etas2.argmax_states())
+            if stream is not None:
+                stream.synchronize()
+        return etas2, t_init2
 
     # ------------------------------------------------------------------ outputs
     def package_s_output(self, cn_s, trace_s, cn_s_reads_df, lambda_fit, losses_g, losses_s):

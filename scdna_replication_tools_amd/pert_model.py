@@ -382,8 +382,8 @@ class pert_infer_scRT():
         n_libs = self.L
         self.timings["prep"] = time.perf_counter() - tic
         # host work that only steps 2/3 need runs on a helper thread while step 1 fits on the
-        # device: the consensus profiles and the step-2 prior, then (during step 2) the
-        # step-3 prior and tau initialisation on a side stream
+        # device: the consensus profiles, the step-2 prior and tau initialisation, then (during
+        # step 2) the step-3 prior and tau initialisation -- device parts on a side stream
         from concurrent.futures import ThreadPoolExecutor
         helper = ThreadPoolExecutor(max_workers=1, thread_name_prefix="pert-prep")
 
@@ -395,10 +395,19 @@ class pert_infer_scRT():
                 return fn(*a)
 
         def priors():
+            t0 = time.perf_counter()
             profiles = prep.consensus_clone_profiles(
                 self.cn_g1, self.cn_state_col, clone_col=self.clone_col, cell_col=self.cell_col,
                 chr_col=self.chr_col, start_col=self.start_col, cn_state_col=self.cn_state_col, keys=inp.keys_g)
-            return profiles, self._build_etas(inp, profiles)
+            etas = self._build_etas(inp, profiles)
+            t1 = time.perf_counter()
+            # step 2's tau initialisation (:790), its device part on a side stream
+            stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+            with (torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()):
+                t_init, _, _ = self._guess_times(inp.reads_s, etas.argmax_states())
+                if stream is not None:
+                    stream.synchronize()
+            return profiles, etas, t_init, (t1 - t0, time.perf_counter() - t1)
 
         fut_priors = helper.submit(on_device, priors)
 
@@ -415,13 +424,12 @@ class pert_infer_scRT():
 
         # ---- step 2: S cells, enumerated (:776-830)
         tic = time.perf_counter()
-        profiles, etas = fut_priors.result()
-        self.timings["prep"] += time.perf_counter() - tic            # the part step 1 did not hide
-        tic = time.perf_counter()
-        t_init, _, _ = self._guess_times(inp.reads_s, etas.argmax_states())
-        # (submitted after the step-2 initialiser: the two never share the per-cell pool)
-        fut_prep3 = helper.submit(on_device, self._prep_step3, inp, profiles) if self.run_step3 else None
+        profiles, etas, t_init, (t_priors, t_guess) = fut_priors.result()
+        # wall time step 1 did not hide (the helper's own durations: timings["helper_*"])
         self.timings["guess_times_s"] = time.perf_counter() - tic
+        self.timings["helper_priors"], self.timings["helper_guess_times_s"] = t_priors, t_guess
+        # (the helper runs its tasks in order: the two tau initialisers never share the pool)
+        fut_prep3 = helper.submit(on_device, self._prep_step3, inp, profiles) if self.run_step3 else None
         ploidy = etas.argmax_states().astype(np.float32).mean(0)
         init2 = init_params(KIND_STEP2, inp.reads_s, inp.libs_s, n_libs, P, K, ploidy=ploidy, t_init=t_init,
                             beta_means=beta_means_fit, seed=self.seed, method=self.init_method)

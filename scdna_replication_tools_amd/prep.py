@@ -350,13 +350,24 @@ def _cell_libraries(cn: pd.DataFrame, keys: TableKeys, library_col: str, cells: 
     the library labels in first-appearance order and one label per pivot cell."""
     lib_code, lib_uniq = _factorize(cn[library_col].to_numpy())
     cc = keys.cell_code
-    ok = cc >= 0
-    pairs = pd.unique(cc[ok] * (len(lib_uniq) + 1) + lib_code[ok])
-    pc, pl = pairs // (len(lib_uniq) + 1), pairs % (len(lib_uniq) + 1)
-    if np.unique(pc).size != pc.size:
-        raise ValueError("a cell belongs to more than one {}".format(library_col))
-    per_cell = np.full(keys.cells.size, -1, np.int64)
-    per_cell[pc] = pl
+    fast = False
+    if getattr(keys, "regular", 0) and lib_code.size == cc.size:
+        # regular table: cell c is rows [c L, (c+1) L); one library per cell is a row compare
+        lc2 = np.asarray(lib_code).reshape(keys.cells.size, keys.regular)
+        if (lc2[:, 0] >= 0).all():
+            if not (lc2 == lc2[:, :1]).all():
+                raise ValueError("a cell belongs to more than one {}".format(library_col))
+            pl = lc2[:, 0].astype(np.int64)
+            per_cell = pl
+            fast = True
+    if not fast:
+        ok = cc >= 0
+        pairs = pd.unique(cc[ok] * (len(lib_uniq) + 1) + lib_code[ok])
+        pc, pl = pairs // (len(lib_uniq) + 1), pairs % (len(lib_uniq) + 1)
+        if np.unique(pc).size != pc.size:
+            raise ValueError("a cell belongs to more than one {}".format(library_col))
+        per_cell = np.full(keys.cells.size, -1, np.int64)
+        per_cell[pc] = pl
     order = pd.unique(pl)                                # first appearance over the (sorted) rows
     sel = pd.Index(keys.cells).get_indexer(cells)
     return [lib_uniq[i] for i in order], lib_uniq[per_cell[sel]]
@@ -397,9 +408,12 @@ def process_input_data(cn_s: pd.DataFrame, cn_g1: pd.DataFrame, input_col="reads
 
     # gc per locus: first row of each locus in the sorted S table
     gcv = cn_s[gc_col].to_numpy(np.float64)
-    okr = ks.valid
-    _, first = np.unique(ks.locus_code[okr], return_index=True)
-    gc_locus = gcv[np.flatnonzero(okr)[first]]
+    if getattr(ks, "regular", 0) and gcv.size == ks.cell_code.size:
+        gc_locus = gcv[:ks.regular]                      # regular table: cell 0's rows, locus order
+    else:
+        okr = ks.valid
+        _, first = np.unique(ks.locus_code[okr], return_index=True)
+        gc_locus = gcv[np.flatnonzero(okr)[first]]
     gkey = pd.MultiIndex.from_arrays([ks.loci_chr.astype(str), ks.loci_start])
     gi = gkey.get_indexer(pd.MultiIndex.from_arrays([ps_r.loci_chr.astype(str), ps_r.loci_start]))
     gc = gc_locus[gi].astype(np.float32)

@@ -175,3 +175,18 @@ def test_consensus_matches_reference_golden():
     assert list(np.asarray(got.index.get_level_values(0)).astype(str)) == list(g["prof_chr"])
     assert (np.asarray(got.index.get_level_values(1)) == g["prof_start"]).all()
     np.testing.assert_array_equal(got.to_numpy(np.float64), g["prof_values"])
+
+
+@pytest.mark.parametrize("complete", [True, False])
+def test_cell_in_two_libraries_is_refused(complete):
+    """get_libraries_tensor (:206-225) asserts one library per cell; both the regular-table
+    path and the general one raise."""
+    s = _table(6, "s", seed=4)
+    g = _table(5, "g", seed=5)
+    c0 = s.cell_id.iloc[0]
+    rows = s.index[s.cell_id == c0]
+    s.loc[rows[:3], "library_id"] = "L_other"
+    if not complete:
+        s = s.drop(index=s.index[s.cell_id == s.cell_id.iloc[-1]][:2])
+    with pytest.raises(ValueError, match="more than one"):
+        prep.process_input_data(s, g)

@@ -744,6 +744,11 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
   __shared__ float s_tab[kDecode ? 1 : kEnum3TabFloats];
 
   const int lane = threadIdx.x;
+#ifdef PERT_ENUM3_STAMPS
+  // diagnostic build only (tools/wave_timeline.py): s_memrealtime at entry, first bin, exit
+  unsigned long long* dbg = (unsigned long long*)st.g_pi + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4;
+  const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
+#endif
   const int N = pr.N, K1 = (K1T == PERT_MAX_K1) ? pr.K1 : K1T, ldn = pr.ldn;
   const int wt = blockIdx.x;
   const int n = wt * 64 + lane;
@@ -836,6 +841,9 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
     }
     // ---- x, eta code and pi logits of bin l into registers; then the copies of bin l+1 and
     // this bin's Adam moments are issued (they land during the NB chains)
+#ifdef PERT_ENUM3_STAMPS
+    if (kStep && lb == 0 && lane == 0) dbg[1] = __builtin_amdgcn_s_memrealtime();
+#endif
     const float x = s_xc[lane];
     const uint32_t code = ((const uint16_t*)(s_xc + 64))[lane];
     float z[P];
@@ -971,6 +979,16 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
     }
   }
   if (kStep && fuse) enum3_fused_tail<K1T>(pr, st, hp, wt, blockIdx.y, lane, fuse == 2);
+#ifdef PERT_ENUM3_STAMPS
+  if (kStep && lane == 0) {
+    dbg[0] = t_entry;
+    dbg[2] = __builtin_amdgcn_s_memrealtime();
+    unsigned int hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    dbg[3] = ((unsigned long long)xcc << 32) | hw;
+  }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------

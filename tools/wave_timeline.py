@@ -1,4 +1,5 @@
-"""Wave timeline of the enumerated pass (diagnostic build, variant 2): per workgroup the
+"""Wave timeline of the enumerated pass (diagnostic builds: variant 2 = variant 0 with stamps;
+VARIANT=3 with PERT_LIB naming a -DPERT_ENUM3_STAMPS build of the three-wave pass): per workgroup the
 s_memrealtime stamps (100 MHz) at entry, first-bin start and exit, plus the XCC / HW ids.
 Prints the launch span, entry / exit spreads and how many waves are resident over time.
 usage: python tools/wave_timeline.py CELLS [SUBDIVIDE]"""
@@ -20,7 +21,7 @@ bm = np.zeros((1, 5)); bm[0, 3] = 0.5
 init = init_params(2, reads, np.zeros(cells, int), 1, 13, 4, ploidy=eta.argmax_states().mean(0),
                    t_init=np.clip(data["tau"].cpu().numpy(), 0.05, 0.95), beta_means=bm, seed=0)
 sh = PertShard(2, reads, data["gc"], np.zeros(cells, int), 1, 13, 4, init, eta=eta, lamb=0.75, beta_means=bm,
-               device=dev, variant=2, bins_per_tile=int(os.environ.get("LT", "0")))
+               device=dev, variant=int(os.environ.get("VARIANT", "2")), bins_per_tile=int(os.environ.get("LT", "0")))
 L = reads.shape[0]
 n_wg = (-(-cells // 64)) * (-(-L // sh.bins_per_tile))
 dbg = torch.zeros(n_wg * 4, dtype=torch.int64, device=dev)

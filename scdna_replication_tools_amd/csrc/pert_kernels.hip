@@ -659,6 +659,9 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
 #ifndef PERT_ENUM3_WAVES
 #define PERT_ENUM3_WAVES 3
 #endif
+#ifndef PERT_ENUM3_PRIO
+#define PERT_ENUM3_PRIO 1            // issue priority falls by quarters of the tile (0: none)
+#endif
 constexpr int kEnum3TabFloats = 192;            // eta table staged in LDS up to this size
 constexpr unsigned kRsrcWord3 = 0x00020000;     // raw buffer resource, gfx9 data format
 
@@ -830,15 +833,19 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
   float sgt = 0.0f, loss = 0.0f, ga = 0.0f;
   const uint32_t voff = lane * 4;
 
+#if PERT_ENUM3_PRIO
   __builtin_amdgcn_s_setprio(3);
+#endif
   for (int l = l0; l < l1; ++l) {
     const int lb = l - l0;
+#if PERT_ENUM3_PRIO
     {
       const int q4 = 4 * lb;
       if (q4 >= nb && q4 - 4 < nb) __builtin_amdgcn_s_setprio(2);
       if (q4 >= 2 * nb && q4 - 4 < 2 * nb) __builtin_amdgcn_s_setprio(1);
       if (q4 >= 3 * nb && q4 - 4 < 3 * nb) __builtin_amdgcn_s_setprio(0);
     }
+#endif
     // ---- x, eta code and pi logits of bin l into registers; then the copies of bin l+1 and
     // this bin's Adam moments are issued (they land during the NB chains)
 #ifdef PERT_ENUM3_STAMPS

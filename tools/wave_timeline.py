@@ -55,3 +55,33 @@ if (~first_round).any():
     mid = (ent > 0.3 * span) & (ex < 0.7 * span)
     if mid.any():
         print("wave dur mid-kernel pct              :", q(dur[mid]))
+
+# where the slow waves are: by bin tile, by cell tile, by SIMD occupancy of their CU
+n_ct = -(-cells // 64)
+by = np.arange(n_wg) // n_ct
+wt = np.arange(n_wg) % n_ct
+hw = (d[:, 3] & 0xffffffff).astype(np.int64)
+simd = (hw >> 4) & 3
+cu = (hw >> 8) & 15
+sh = (hw >> 12) & 1
+se = (hw >> 13) & 7
+cu_key = xcc * 1000 + se * 100 + sh * 20 + cu
+_, cu_idx, cu_cnt = np.unique(cu_key, return_inverse=True, return_counts=True)
+waves_on_cu = cu_cnt[cu_idx]
+simd_key = cu_key * 4 + simd
+_, s_idx, s_cnt = np.unique(simd_key, return_inverse=True, return_counts=True)
+waves_on_simd = s_cnt[s_idx]
+print("CUs used {} (waves per CU: {})".format(len(cu_cnt), np.bincount(cu_cnt)))
+for k in sorted(set(waves_on_simd.tolist())):
+    m = waves_on_simd == k
+    print("waves sharing the SIMD {}: {} waves, dur p50 {:.1f} mean {:.1f}".format(k, m.sum(), np.median(dur[m]), dur[m].mean()))
+for k in sorted(set(waves_on_cu.tolist())):
+    m = waves_on_cu == k
+    print("waves on the CU {}: {} waves, dur p50 {:.1f} mean {:.1f}".format(k, m.sum(), np.median(dur[m]), dur[m].mean()))
+nbt = by.max() + 1
+for q in range(5):
+    m = (by >= q * nbt / 5) & (by < (q + 1) * nbt / 5)
+    print("bin tiles quintile {}: dur mean {:.1f}".format(q, dur[m].mean()))
+for q in range(5):
+    m = (wt >= q * n_ct / 5) & (wt < (q + 1) * n_ct / 5)
+    print("cell tiles quintile {}: dur mean {:.1f}".format(q, dur[m].mean()))

@@ -6,7 +6,7 @@ A ``PertShard`` owns every buffer of one fit (step 1, 2 or 3 of reference
 * inputs: reads (L, N) fp32, gc features (L, K+1), library index (N,), the CN
   prior eta as a code book (uint16 codes (L, N) + table) for steps 2/3, the
   observed cn / rep (uint8) for step 1;
-* the pi logits and their Adam moments as (L, P, N) planes (steps 2/3);
+* the pi logits and their Adam moments as wave tiles [N/64][L][P][64] (steps 2/3);
 * the packed non-pi parameters (layout ``pert_layout`` of include/pert_hip.h),
   their Adam moments and gradients.
 

@@ -175,14 +175,14 @@ class pert_infer_scRT():
         self._inp = None
 
     # ------------------------------------------------------------------ prep (host)
-    def _prepare(self) -> prep.PertInputs:
+    def _prepare(self, on_g1_sorted=None) -> prep.PertInputs:
         """pert_model.py:133-191, vectorised (prep.process_input_data): sorts and filters
         self.cn_s / self.cn_g1 like the reference and returns the tensor inputs."""
         if self._inp is None:
             self.cn_s, self.cn_g1, inp = prep.process_input_data(
                 self.cn_s, self.cn_g1, input_col=self.input_col, gc_col=self.gc_col, cell_col=self.cell_col,
                 library_col=self.library_col, chr_col=self.chr_col, start_col=self.start_col,
-                cn_state_col=self.cn_state_col)
+                cn_state_col=self.cn_state_col, on_g1_sorted=on_g1_sorted)
             self.L = len(inp.library_ids)
             self._inp = inp
         return self._inp
@@ -377,13 +377,10 @@ class pert_infer_scRT():
             torch.cuda.set_device(self.device)
         if self.tau_init_method != 'sklearn':
             prewarm_pool(self.n_jobs if self.n_jobs != 1 else -1)   # overlaps prep and step 1
-        tic = time.perf_counter()
-        inp = self._prepare()
-        n_libs = self.L
-        self.timings["prep"] = time.perf_counter() - tic
-        # host work that only steps 2/3 need runs on a helper thread while step 1 fits on the
-        # device: the consensus profiles, the step-2 prior and tau initialisation, then (during
-        # step 2) the step-3 prior and tau initialisation -- device parts on a side stream
+        # host work that only steps 2/3 need runs on a helper thread: the consensus profiles as
+        # soon as the G1/2 table is sorted (while the S table is prepared), the step-2 prior and
+        # tau initialisation while step 1 fits, then (during step 2) the step-3 prior and tau
+        # initialisation -- device parts on a side stream
         from concurrent.futures import ThreadPoolExecutor
         helper = ThreadPoolExecutor(max_workers=1, thread_name_prefix="pert-prep")
 
@@ -394,11 +391,24 @@ class pert_infer_scRT():
             with torch.cuda.device(self.device):
                 return fn(*a)
 
-        def priors():
+        def consensus(cn_g1, keys_g):
             t0 = time.perf_counter()
-            profiles = prep.consensus_clone_profiles(
-                self.cn_g1, self.cn_state_col, clone_col=self.clone_col, cell_col=self.cell_col,
-                chr_col=self.chr_col, start_col=self.start_col, cn_state_col=self.cn_state_col, keys=inp.keys_g)
+            prof = prep.consensus_clone_profiles(
+                cn_g1, self.cn_state_col, clone_col=self.clone_col, cell_col=self.cell_col,
+                chr_col=self.chr_col, start_col=self.start_col, cn_state_col=self.cn_state_col, keys=keys_g)
+            return prof, time.perf_counter() - t0
+
+        fut_prof = []
+        tic = time.perf_counter()
+        inp = self._prepare(on_g1_sorted=lambda t, k: fut_prof.append(helper.submit(on_device, consensus, t, k)))
+        if not fut_prof:                       # inputs prepared before this call: consensus now
+            fut_prof.append(helper.submit(on_device, consensus, self.cn_g1, inp.keys_g))
+        n_libs = self.L
+        self.timings["prep"] = time.perf_counter() - tic
+
+        def priors():
+            profiles, t_cons = fut_prof[0].result()         # ran earlier on this same thread
+            t0 = time.perf_counter()
             etas = self._build_etas(inp, profiles)
             t1 = time.perf_counter()
             # step 2's tau initialisation (:790), its device part on a side stream
@@ -407,7 +417,7 @@ class pert_infer_scRT():
                 t_init, _, _ = self._guess_times(inp.reads_s, etas.argmax_states())
                 if stream is not None:
                     stream.synchronize()
-            return profiles, etas, t_init, (t1 - t0, time.perf_counter() - t1)
+            return profiles, etas, t_init, (t_cons + t1 - t0, time.perf_counter() - t1)
 
         fut_priors = helper.submit(on_device, priors)
 

@@ -375,21 +375,25 @@ def _cell_libraries(cn: pd.DataFrame, keys: TableKeys, library_col: str, cells: 
 
 def process_input_data(cn_s: pd.DataFrame, cn_g1: pd.DataFrame, input_col="reads", gc_col="gc",
                        cell_col="cell_id", library_col="library_id", chr_col="chr", start_col="start",
-                       cn_state_col="state"):
+                       cn_state_col="state", on_g1_sorted=None):
     """pert_model.py:133-191 (the unused rt prior aside).  Returns the sorted,
-    NaN-filtered long tables and a ``PertInputs``."""
+    NaN-filtered long tables and a ``PertInputs``.  ``on_g1_sorted(table, keys)`` is called
+    with the sorted G1/2 table as soon as it exists (work that needs only it can start while
+    the S table is still being prepared)."""
     from concurrent.futures import ThreadPoolExecutor
 
-    def table(cn):
+    def table(cn, hook=None):
         # the two tables are independent: sorted and pivoted on two threads (the numpy
         # passes release the GIL; the object-column passes interleave)
         cn, k = _sorted_table(cn, cell_col, chr_col, start_col, notna_col=input_col)
+        if hook is not None:
+            hook(cn, k)
         r = drop_incomplete_loci(pivot_cells_by_loci(cn, input_col, cell_col, chr_col, start_col, k))
         st = drop_incomplete_loci(pivot_cells_by_loci(cn, cn_state_col, cell_col, chr_col, start_col, k))
         return cn, k, r, st
 
     with ThreadPoolExecutor(max_workers=2) as ex:
-        fg, fs = ex.submit(table, cn_g1), ex.submit(table, cn_s)
+        fg, fs = ex.submit(table, cn_g1, on_g1_sorted), ex.submit(table, cn_s)
         cn_g1, kg, pg_r, pg_s = fg.result()
         cn_s, ks, ps_r, ps_s = fs.result()
     assert pg_s.values.shape == pg_r.values.shape                      # :153

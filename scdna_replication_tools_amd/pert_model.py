@@ -169,6 +169,10 @@ class pert_infer_scRT():
         self.init_method = init_method
         self.dirichlet_mode = dirichlet_mode
         self.n_jobs = n_jobs
+        # worker processes of the batched tau initialiser's per-cell path (its fragile cells):
+        # the affinity cores (at most 16) unless n_jobs > 1 names a count; tau_pool_jobs=1 runs
+        # them in this process
+        self.tau_pool_jobs = n_jobs if n_jobs > 1 else -1
         self.tau_init_method = tau_init_method
         self.timings = {}
         self.iters = {}
@@ -289,7 +293,7 @@ class pert_infer_scRT():
     def _guess_times(self, reads, cn_states):
         if self.tau_init_method == 'sklearn':
             return prep.guess_times(reads, cn_states, self.upsilon, self.n_jobs)
-        return guess_times_batched(reads, cn_states, self.upsilon, device=self.device)
+        return guess_times_batched(reads, cn_states, self.upsilon, device=self.device, n_jobs=self.tau_pool_jobs)
 
     def make_gc_features(self, x):
         """pert_model.py:460-463: columns [x^K, ..., x, 1]."""
@@ -376,7 +380,7 @@ class pert_infer_scRT():
         if self.device.type == "cuda" and self.device.index is not None:
             torch.cuda.set_device(self.device)
         if self.tau_init_method != 'sklearn':
-            prewarm_pool(self.n_jobs if self.n_jobs != 1 else -1)   # overlaps prep and step 1
+            prewarm_pool(self.tau_pool_jobs)           # overlaps prep and step 1 (no-op for 1)
         # host work that only steps 2/3 need runs on a helper thread: the consensus profiles as
         # soon as the G1/2 table is sorted (while the S table is prepared), the step-2 prior and
         # tau initialisation while step 1 fits, then (during step 2) the step-3 prior and tau

@@ -116,10 +116,14 @@ def _fit(**extra):
     s, g = _tables()
     m = pert_infer_scRT(s, g, input_col='reads', clone_col='clone_id', cn_prior_method='g1_clones',
                         max_iter=120, min_iter=30, max_iter_step1=80, max_iter_step3=60, **extra)
+    m.tau_pool_jobs = 1                   # the ranks' per-cell tau path in-process (no worker pools)
     return m.run_pert_model()
 
 
 def _api_worker(rank, world, port, out_dir):
+    import faulthandler
+    import sys
+    faulthandler.dump_traceback_later(150, exit=True, file=sys.stderr)   # a hung rank shows where
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{}".format(port), rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)

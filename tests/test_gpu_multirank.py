@@ -123,7 +123,7 @@ def _fit(**extra):
 def _api_worker(rank, world, port, out_dir):
     import faulthandler
     import sys
-    faulthandler.dump_traceback_later(150, exit=True, file=sys.stderr)   # a hung rank shows where
+    faulthandler.dump_traceback_later(170, exit=True, file=sys.stderr)   # a hung rank shows where
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{}".format(port), rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
@@ -143,7 +143,15 @@ def test_run_pert_model_two_ranks_match_single_rank(tmp_path):
     cell-sharded over the two ranks with the all-reduce per step, every rank returns the full
     output tables -- equal to the single-process fit's (losses to summation-order noise,
     calls and per-cell sites)."""
-    mp.spawn(_api_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    import time
+    ctx = mp.spawn(_api_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=False)
+    deadline = time.time() + 200          # bounded: a hung rank fails the test instead of the suite
+    while not ctx.join(timeout=5):
+        if time.time() > deadline:
+            for p in ctx.processes:
+                if p.is_alive():
+                    p.kill()
+            pytest.fail("the two ranks did not finish within 200 s")
     r = [torch.load(str(tmp_path / "api{}.pt".format(i)), weights_only=True) for i in range(2)]
     cn_s, supp_s, cn_g, supp_g = _fit()
     cols = ["model_cn_state", "model_rep_state", "model_tau", "model_u", "model_rho"]

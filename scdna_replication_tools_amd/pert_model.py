@@ -379,6 +379,10 @@ class pert_infer_scRT():
         dd = _Dist(self._group)
         if self.device.type == "cuda" and self.device.index is not None:
             torch.cuda.set_device(self.device)
+        if dd.world > 1 and self.n_jobs <= 1:
+            # every rank runs the tau initialiser on all cells; worker processes started from a
+            # rank (whose __main__ may be a launcher's) are not safe to assume -- in-process
+            self.tau_pool_jobs = 1
         if self.tau_init_method != 'sklearn':
             prewarm_pool(self.tau_pool_jobs)           # overlaps prep and step 1 (no-op for 1)
         # host work that only steps 2/3 need runs on a helper thread: the consensus profiles as

@@ -191,6 +191,10 @@ class pert_infer_scRT():
             self._inp = inp
         return self._inp
 
+    def _long_rows(self) -> int:
+        """Rows of the two input tables (cells x bins), before any preparation."""
+        return int(len(self.cn_s)) + int(len(self.cn_g1))
+
     def _axes(self, cells, keys=None) -> PivotAxes:
         inp = self._prepare()
         return PivotAxes(inp.loci_chr, inp.loci_start, cells, self.chr_col, self.start_col, self.cell_col, keys)
@@ -383,8 +387,9 @@ class pert_infer_scRT():
             # every rank runs the tau initialiser on all cells; worker processes started from a
             # rank (whose __main__ may be a launcher's) are not safe to assume -- in-process
             self.tau_pool_jobs = 1
-        if self.tau_init_method != 'sklearn':
-            prewarm_pool(self.tau_pool_jobs)           # overlaps prep and step 1 (no-op for 1)
+        if self.tau_init_method != 'sklearn' and self._long_rows() >= 10 ** 7:
+            # genome-scale inputs: start the per-cell worker pool now, overlapping prep and step 1
+            prewarm_pool(self.tau_pool_jobs)           # (no-op for 1)
         # host work that only steps 2/3 need runs on a helper thread: the consensus profiles as
         # soon as the G1/2 table is sorted (while the S table is prepared), the step-2 prior and
         # tau initialisation while step 1 fits, then (during step 2) the step-3 prior and tau

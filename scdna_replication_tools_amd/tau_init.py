@@ -322,12 +322,12 @@ def prewarm_pool(n_jobs: int = -1):
     th.start()
 
 
-def _pool_ready(n_jobs: int) -> bool:
+def _pool_state(n_jobs: int) -> str:
+    """'none' (no background start), 'warming' or 'ready' -- without waiting."""
     th = _WARM.get(_pool_size(n_jobs))
     if th is None:
-        return False
-    th.join()                              # never two executors being built at once
-    return True
+        return "none"
+    return "warming" if th.is_alive() else "ready"
 
 
 def guess_times_batched(reads: np.ndarray, cn_states: np.ndarray, upsilon: float = 6, device=None,
@@ -355,8 +355,13 @@ def guess_times_batched(reads: np.ndarray, cn_states: np.ndarray, upsilon: float
         from .prep import manhattan_binarization
         cols = norm[:, torch.as_tensor(redo, device=dev)].cpu().numpy()
         jobs = [cols[:, j].reshape(-1, 1) for j in range(redo.size)]
-        warm = _pool_ready(n_jobs)
-        if n_jobs != 1 and (redo.size > 64 or (warm and redo.size > 4)):
+        # worker processes only where the per-cell fits outweigh their start-up: more than 64
+        # genome-scale cells' worth of bins, or a few cells once the pool is already warm
+        state = _pool_state(n_jobs)
+        big = redo.size * L > 64 * 5451
+        if n_jobs != 1 and redo.size > 4 and (big or state == "ready"):
+            if state == "warming":
+                _WARM[_pool_size(n_jobs)].join()    # never two executors being built at once
             from joblib import Parallel, delayed
             res = Parallel(n_jobs=_pool_size(n_jobs))(delayed(manhattan_binarization)(c) for c in jobs)
         else:

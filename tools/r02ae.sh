@@ -6,5 +6,7 @@ timeout -k 10 600 python bench.py --fullfit-c1 > gpurun_out/r02ae_fullfit_c1.log
 tail -1 gpurun_out/r02ae_fullfit_c1.log
 timeout -k 10 600 python tools/fullfit_bench.py --config c2 --cpu-sample-cells 0 > gpurun_out/r02ae_fullfit_c2.log 2>&1 || exit $?
 tail -1 gpurun_out/r02ae_fullfit_c2.log
-timeout -k 10 600 python tools/fullfit_bench.py --config c3 --cpu-sample-cells 64 > gpurun_out/r02ae_fullfit_c3.log 2>&1 || exit $?
+timeout -k 10 600 python tools/fullfit_bench.py --config c3 --cpu-sample-cells 0 > gpurun_out/r02ae_fullfit_c3.log 2>&1 || exit $?
 tail -1 gpurun_out/r02ae_fullfit_c3.log
+timeout -k 10 600 python tools/fullfit_bench.py --config c4 --cpu-sample-cells 0 > gpurun_out/r02ae_fullfit_c4.log 2>&1 || exit $?
+tail -1 gpurun_out/r02ae_fullfit_c4.log

@@ -2,6 +2,7 @@
 reference's manhattan_binarization (prep.manhattan_binarization, pert_model.py:364-423)."""
 import numpy as np
 import pytest
+import torch
 
 from scdna_replication_tools_amd import prep, tau_init
 
@@ -53,3 +54,25 @@ def test_batched_guess_times_matches_sklearn_per_cell(seed, L):
     np.testing.assert_array_equal(a_b, a_r)
     np.testing.assert_allclose(a_b + b_b, 6.0, rtol=1e-6)
     assert len(tau_init.guess_times_batched.last_fragile) < reads.shape[1]    # not all through sklearn
+
+
+def test_fragile_cells_same_on_the_worker_pool_and_in_process(monkeypatch):
+    """The fragile cells' per-cell path gives the same t_init in-process and on a warm worker
+    pool (the paths guess_times_batched picks by problem size and pool state)."""
+    from scdna_replication_tools_amd import tau_init
+    from scdna_replication_tools_amd.simulator import simulate
+    sim = simulate(n_s=12, n_g=12, n_bins=300, num_reads=183 * 300, seed=2)
+    real = tau_init.binarization_fraction
+
+    def all_fragile(x, return_fragile=False, return_minor=False):
+        f, d, n = real(x, return_fragile=True, return_minor=True)
+        return f, torch.ones_like(d), torch.zeros_like(n)
+
+    monkeypatch.setattr(tau_init, "binarization_fraction", all_fragile)
+    t1 = tau_init.guess_times_batched(sim.reads_s, sim.cn_s, 6, device="cpu", n_jobs=1)[0]
+    assert len(tau_init.guess_times_batched.last_fragile) == 12
+    tau_init.prewarm_pool(2)
+    tau_init._WARM[2].join()
+    assert tau_init._pool_state(2) == "ready"
+    t2 = tau_init.guess_times_batched(sim.reads_s, sim.cn_s, 6, device="cpu", n_jobs=2)[0]
+    np.testing.assert_array_equal(t1, t2)

@@ -250,7 +250,7 @@ def main():
     ap.add_argument("--fit", default="step2", choices=["step1", "step2", "step3"],
                     help="which SVI fit's step to time (the metric is step 2's)")
     ap.add_argument("--variant", type=int, default=3, help="enumerated-pass kernel: 3 three-wave streamed (default), "
-                    "0 two-wave LDS-DMA, 1 register pipeline")
+                    "0 two-wave LDS-DMA")
     ap.add_argument("--fused", action="store_true", help="variant 3: one launch per step (pert_enum_step)")
     ap.add_argument("--no-fused", action="store_true", help="(the default) separate finalize / adam launches")
     ap.add_argument("--cells", type=int, default=0, help="override the config's cell count (per job)")
@@ -371,7 +371,7 @@ def main():
         achieved = bpc * local_cb / (kern_ms * 1e-3) / 1e9
         kname = ("obs_kernel" if step1 else
                  "enum3_kernel<13, 0, 5>" if args.variant == 3 else
-                 "enum_dma_kernel<13, 0, 5>" if args.variant != 1 else "enum_kernel<13, 0>")
+                 "enum_dma_kernel<13, 0, 5>")
         traffic, valu = None, None
         if os.path.exists(args.pmc) and args.fit == "step2":
             try:
@@ -395,7 +395,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
                          "kernel": ("obs_kernel" if step1 else
                                     "enum3_kernel<13, STEP, 5>" if args.variant == 3 else
-                                    "enum_dma_kernel<13, STEP, 5>" if args.variant != 1 else "enum_kernel<13, STEP>"),
+                                    "enum_dma_kernel<13, STEP, 5>"),
                          "kernel_ms": kern_ms,
                          "bytes_per_cellbin": bpc,
                          # PMC (profiles/pmc_traffic.json, tools/profile.sh): VALU issue fraction of

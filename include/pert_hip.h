@@ -116,9 +116,10 @@ typedef struct {
   double* blk_part;
   double* cellblk_part;
   int32_t bins_per_tile;           /* LT; 0 = library default */
-  int32_t variant;                 /* enumerated-pass kernel: 0 LDS-DMA streamed, 1 register pipelined,
+  int32_t variant;                 /* enumerated-pass kernel: 0 LDS-DMA streamed (two waves per SIMD),
                                       2 = variant 0 + wave timeline stamps into g_pi (diagnostic, STEP mode),
-                                      3 = three waves per SIMD, online logsumexp (pert_enum_step) */
+                                      3 = three waves per SIMD, online logsumexp (pert_enum_step);
+                                      anything else (1 was retired in round 3) -> PERT_E_ARG */
   /* Device-side SVI loop control (the loop of pert_model.py:742-758, :800-816, :867-883).
    * loop_ctl == NULL disables it.  Otherwise pert_adam records the loss of iteration
    * `step` (after the cross-rank all-reduce) into loop_rec and evaluates the reference's

@@ -6,7 +6,7 @@ clones and runs ``pert_infer_scRT`` on the GPU (scdna_replication_tools_amd.infe
 """
 from scdna_replication_tools_amd.cncluster import kmeans_cluster  # noqa: F401
 from scdna_replication_tools_amd.infer_scRT import assign_s_to_clones, scRT  # noqa: F401
-from scdna_replication_tools_amd.pert_model import pert_infer_scRT  # noqa: F401
+from scdna_replication_tools.pert_model import pert_infer_scRT  # noqa: F401  (the reference's import: logging set-up)
 from scdna_replication_tools.compute_consensus_clone_profiles import compute_consensus_clone_profiles  # noqa: F401
 
 __all__ = ["scRT"]

@@ -2,7 +2,8 @@
 //
 // One SVI step of reference pert_model.py (svi_s.step at :801, svi.step at :743,
 // svi_s2.step at :868) becomes:
-//   enum_kernel / obs_kernel   one pass over every (bin, cell): forward, analytic backward,
+//   enum3_kernel (default) / enum_dma_kernel (variant 0) / obs_kernel (step 1)
+//                              one pass over every (bin, cell): forward, analytic backward,
 //                              fused Adam on the (L, P, N) pi logits, reduction partials
 //   finalize_kernel            per-cell sums + u / betas / tau priors (:589-603),
 //                              per-bin sums for rho (:572-574), and in its last block
@@ -10,10 +11,10 @@
 //   adam_kernel                Adam on the packed non-pi params
 // All reductions are fixed-order (no float atomics), so a rerun is bit-identical.
 //
-// Work decomposition: workgroup = 256 cells (4 waves, one cell per lane) x LT bins.
-// Lanes walk their bins in order; per-cell partial sums stay in registers, per-bin
-// sums are wave shuffles + LDS.  Every HBM access of the (L, N) / (L, P, N) tensors is a
-// 256-byte contiguous wave access (cells are the fastest axis).
+// Work decomposition of the enumerated passes: one wave per workgroup = 64 cells (one per
+// lane) x LT bins (obs_kernel: 256 cells x LT bins).  Lanes walk their bins in order;
+// per-cell partial sums stay in registers, per-bin sums are wave shuffles.  Every HBM access
+// of the (L, N) / (L, P, N) tensors is a contiguous wave access (cells are the fastest axis).
 
 #include "../../include/pert_hip.h"
 #include "pert_math.h"
@@ -72,196 +73,6 @@ __device__ __forceinline__ bool loop_stopped(const pert_state& st) {
   if (st.loop_ctl == nullptr) return false;
   const int s = *(volatile const int32_t*)st.loop_ctl;
   return s >= 0 && s < st.step;
-}
-
-// ------------------------------------------------------------------------------------------
-// Enumerated pass (steps 2/3).  MODE: PERT_MODE_STEP / PERT_MODE_GRAD / PERT_MODE_DECODE.
-template <int P, int MODE>
-__global__ void __launch_bounds__(kBlock, 2) enum_kernel(pert_problem pr, pert_state st,
-                                                       pert_adam_hparams hp) {
-  constexpr bool kDecode = MODE == PERT_MODE_DECODE;
-  if (MODE == PERT_MODE_STEP && loop_stopped(st)) return;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int N = pr.N, K1 = pr.K1;
-  const int n = blockIdx.x * kBlock + tid;
-  const bool valid = n < N;
-  const int LT = st.bins_per_tile;
-  const int l0 = blockIdx.y * LT;
-  const int l1 = min(pr.L, l0 + LT);
-  const bool frozen = pr.kind == PERT_KIND_STEP3;
-  const pert_layout lay = st.lay;
-
-  __shared__ float s_bin[kWaves][kMaxLT];
-
-  const float a_val = frozen ? pr.a_fixed : fexp(st.params[lay.off_a]);
-  const float c0 = (1.0f - pr.lamb) / pr.lamb;
-
-  float u = 0.0f, tau = 0.5f;
-  float beta[PERT_MAX_K1];
-#pragma unroll
-  for (int k = 0; k < PERT_MAX_K1; ++k) beta[k] = 0.0f;
-  if (valid) {
-    u = st.params[lay.off_u + n];
-#pragma unroll
-    for (int k = 0; k < PERT_MAX_K1; ++k)
-      if (k < K1) beta[k] = st.params[lay.off_beta + k * N + n];
-    float dm;
-    tau = clipped_sigmoid(st.params[lay.off_tau + n], &dm);
-  }
-  const float ucc = u * c0;
-
-  float acc[PERT_MAX_K1];
-#pragma unroll
-  for (int k = 0; k < PERT_MAX_K1; ++k) acc[k] = 0.0f;
-  float accT = 0.0f, loss = 0.0f, ga = 0.0f;
-
-  const float* __restrict__ reads = pr.reads;
-  const uint16_t* __restrict__ codes = pr.eta_code;
-  const float* __restrict__ etab = pr.eta_table;
-  float* __restrict__ zp = st.z_pi;
-  float* __restrict__ mp = st.m_pi;
-  float* __restrict__ vp = st.v_pi;
-  float* __restrict__ gp = st.g_pi;
-  // (L, P, N) state in wave tiles [ldn/64][L][P][64]: one wave's P planes of a bin are
-  // one contiguous P*256-byte run (consecutive bins adjacent), so a lane needs one
-  // address per bin and the planes are immediate offsets (k * 256 B).
-  const int ldn = pr.ldn;
-  const size_t bin_stride = (size_t)P * 64;
-  const size_t toff = (size_t)(n >> 6) * pr.L * P * 64 + lane;
-
-  // Register software pipeline: the reads / eta code / pi logits of bin l+1 are
-  // loaded while bin l computes (one bin of special-function work hides the HBM
-  // latency); the Adam moments of bin l are loaded at the top of its iteration.
-  // Rows are padded to ldn (multiple of 256) so every lane of a launched workgroup
-  // may load; only valid lanes store or accumulate.
-  float xq = 0.0f;
-  uint32_t cq = 0;
-  float zq[P];
-#pragma unroll
-  for (int k = 0; k < P; ++k) zq[k] = 0.0f;
-  if (l0 < l1) {
-    xq = reads[(size_t)l0 * ldn + n];
-    cq = codes[(size_t)l0 * ldn + n];
-    const float* zt = zp + (size_t)l0 * bin_stride + toff;
-#pragma unroll
-    for (int k = 0; k < P; ++k) zq[k] = zt[k * 64];
-  }
-
-  for (int l = l0; l < l1; ++l) {
-    float rho;
-    if (frozen) {
-      rho = pr.rho_fixed[l];
-    } else {
-      float dm;
-      rho = clipped_sigmoid(st.params[lay.off_rho + l], &dm);
-    }
-    float g[PERT_MAX_K1];
-#pragma unroll
-    for (int k = 0; k < PERT_MAX_K1; ++k) g[k] = (k < K1) ? pr.gcf[l * K1 + k] : 0.0f;
-    float gt = 0.0f;
-    const size_t ln = (size_t)l * ldn + n;
-    const size_t tile = (size_t)l * bin_stride + toff;
-    const float x = xq;
-    const uint32_t code = cq;
-    float z[P];
-#pragma unroll
-    for (int k = 0; k < P; ++k) z[k] = zq[k];
-    if (l + 1 < l1) {
-      xq = reads[ln + ldn];
-      cq = codes[ln + ldn];
-      const float* zt = zp + tile + bin_stride;
-#pragma unroll
-      for (int k = 0; k < P; ++k) zq[k] = zt[k * 64];
-    }
-    float mm[P], vv[P];
-    if (MODE == PERT_MODE_STEP) {
-      const float* mt = mp + tile;
-      const float* vt = vp + tile;
-#pragma unroll
-      for (int k = 0; k < P; ++k) { mm[k] = mt[k * 64]; vv[k] = vt[k * 64]; }
-    }
-    const float invx = x > 0.0f ? frcp(x) : 0.0f;
-    float dot = 0.0f;
-#pragma unroll
-    for (int k = 0; k < PERT_MAX_K1; ++k) dot += beta[k] * g[k];
-    const float omega = fexp(dot);                         // pert_model.py:633
-    const float D = ucc * omega;                           // :636-640 (delta = chi D)
-    const float t = tau - rho;                             // :616
-    const float phi = frcp(1.0f + fexp(-a_val * t));       // :619
-    EnumFwd<P> o;
-    enum_forward<P, !kDecode, kDecode>(x, invx, z, pr.log1m_lam, D, phi, o);
-    if (kDecode) {
-      if (valid) {
-        st.cn_out[ln] = (uint8_t)(o.argmax % P);
-        st.rep_out[ln] = (uint8_t)(o.argmax / P);
-      }
-    } else {
-      const float* row = etab + (size_t)code * (P + 1);
-      float em1[P];
-#pragma unroll
-      for (int k = 0; k < P; ++k) em1[k] = row[k];
-      const float S1 = row[P];
-      float gz[P];
-      const float dirv = enum_tail<P>(o, z, em1, S1, gz);
-      if (valid) {
-        loss += o.E + dirv;
-        gt = o.gt;
-        accT += a_val * o.gt;
-        ga += t * o.gt;
-        const float ge = o.gD * omega;
-#pragma unroll
-        for (int k = 0; k < PERT_MAX_K1; ++k) acc[k] += ge * g[k];
-        if (MODE == PERT_MODE_STEP) {
-          float* zt = zp + tile;
-          float* mt = mp + tile;
-          float* vt = vp + tile;
-#pragma unroll
-          for (int k = 0; k < P; ++k) {
-            const float gl = -gz[k];                        // d(-ELBO)/dz
-            const float m1 = hp.beta1 * mm[k] + (1.0f - hp.beta1) * gl;
-            const float v1 = hp.beta2 * vv[k] + (1.0f - hp.beta2) * gl * gl;
-            const float denom = __builtin_sqrtf(v1) * hp.inv_bc2_sqrt + hp.eps;
-            zt[k * 64] = z[k] - hp.step_size * m1 * frcp(denom);
-            mt[k * 64] = m1;
-            vt[k * 64] = v1;
-          }
-        } else {
-          float* gt_ = gp + tile;
-#pragma unroll
-          for (int k = 0; k < P; ++k) gt_[k * 64] = -gz[k];
-        }
-      }
-    }
-    if (!kDecode && !frozen) {
-      const float ws = wave_sum(gt);
-      if (lane == 0) s_bin[wave][l - l0] = ws;
-    }
-  }
-  if (kDecode) return;
-
-  __syncthreads();
-  if (!frozen && tid < l1 - l0) {
-    float s = 0.0f;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) s += s_bin[w][tid];
-    st.bin_part[(size_t)blockIdx.x * pr.L + l0 + tid] = s;
-  }
-  if (valid) {
-    float* cp = st.cell_part + (size_t)blockIdx.y * (K1 + 1) * N + n;
-#pragma unroll
-    for (int k = 0; k < PERT_MAX_K1; ++k)
-      if (k < K1) cp[(size_t)k * N] = acc[k];
-    cp[(size_t)K1 * N] = accT;
-  }
-  // ELBO and d/da sums of each 64-cell wave: blk_part[bt][ldn/64] (read by the finalize
-  // block of that cell tile)
-  const double bl = wave_sum_d((double)loss);
-  const double bga = wave_sum_d((double)ga);
-  if (lane == 0) {
-    double* bp = st.blk_part + ((size_t)blockIdx.y * (ldn / 64) + (n >> 6)) * kBlkSlots;
-    bp[0] = bl;
-    bp[1] = bga;
-  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2019,19 +1830,20 @@ size_t dma_lds_bytes(int P, int mode, const pert_state& st, const pert_problem& 
   return sizeof(float) * (size_t)(2 * SF + (mode == PERT_MODE_STEP ? 2 * ZF : 0) + lt + lt * (pr.K1 + 1) + tab);
 }
 
-// cells per tile of the enumerated pass: 64 for the LDS-DMA kernel (variant 0), 256 otherwise
-int enum_cell_tile(const pert_state* st) { return st->variant != 1 ? 64 : kBlock; }
-// cell tiles launched: only tiles holding at least one real cell (the padding of ldn up to a
-// multiple of 256 is never visited by the 64-cell LDS-DMA tiles)
+// cell tiles launched (64 cells each): only tiles holding at least one real cell (the padding
+// of ldn up to a multiple of 256 is never visited)
 int enum_cell_tiles(const pert_problem* pr, const pert_state* st) {
-  const int ct = enum_cell_tile(st);
-  return st->variant != 1 ? (pr->N + ct - 1) / ct : pr->ldn / ct;
+  (void)st;
+  return (pr->N + 63) / 64;
 }
+
+// the enumerated-pass variants this library carries: 0 (LDS-DMA, two waves per SIMD),
+// 2 (its wave-timeline diagnostic build) and 3 (three waves per SIMD, the default)
+bool variant_ok(int v) { return v == 0 || v == 2 || v == 3; }
 
 template <int MODE>
 int launch_enum_mode(int P, dim3 grid, const pert_problem& pr, const pert_state& st,
                      const pert_adam_hparams& hp, hipStream_t s, int fuse = 0) {
-  const bool dma = st.variant != 1;
   const bool v3 = st.variant == 3;
   switch (P) {
 #define PERT_CASE(PP)                                                                             \
@@ -2040,11 +1852,10 @@ int launch_enum_mode(int P, dim3 grid, const pert_problem& pr, const pert_state&
       hipLaunchKernelGGL((enum3_kernel<PP, MODE, 5>), grid, dim3(64), 0, s, pr, st, hp, fuse);    \
     else if (v3)                                                                                  \
       hipLaunchKernelGGL((enum3_kernel<PP, MODE, PERT_MAX_K1>), grid, dim3(64), 0, s, pr, st, hp, fuse); \
-    else if (dma && pr.K1 == 5)                                                                   \
+    else if (pr.K1 == 5)                                                                          \
       hipLaunchKernelGGL((enum_dma_kernel<PP, MODE, 5>), grid, dim3(64), dma_lds_bytes(PP, MODE, st, pr), s, pr, st, hp); \
-    else if (dma)                                                                                 \
+    else                                                                                          \
       hipLaunchKernelGGL((enum_dma_kernel<PP, MODE, PERT_MAX_K1>), grid, dim3(64), dma_lds_bytes(PP, MODE, st, pr), s, pr, st, hp); \
-    else hipLaunchKernelGGL((enum_kernel<PP, MODE>), grid, dim3(kBlock), 0, s, pr, st, hp);       \
     break;
     PERT_ALL_P_CASES
 #undef PERT_CASE
@@ -2153,8 +1964,9 @@ int pert_auto_bins_per_tile(const pert_problem* prob, int32_t variant, int32_t* 
   if (!prob || !out || prob->L <= 0 || prob->ldn <= 0 || prob->P < PERT_MIN_P || prob->P > PERT_MAX_P ||
       prob->K1 < 1 || prob->K1 > PERT_MAX_K1)
     return PERT_E_ARG;
+  if (!variant_ok(variant)) return PERT_E_ARG;
   *out = kDefaultLT;
-  if (variant == 1 || prob->kind == PERT_KIND_STEP1) return PERT_OK;
+  if (prob->kind == PERT_KIND_STEP1) return PERT_OK;
   int dev = 0, ncu = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -2207,7 +2019,7 @@ int pert_auto_bins_per_tile(const pert_problem* prob, int32_t variant, int32_t* 
 
 int pert_enum_pass(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
                    int32_t mode, hipStream_t stream) {
-  if (!problem_ok(prob) || !st || !hp) return PERT_E_ARG;
+  if (!problem_ok(prob) || !st || !hp || !variant_ok(st->variant)) return PERT_E_ARG;
   if (prob->kind != PERT_KIND_STEP2 && prob->kind != PERT_KIND_STEP3) return PERT_E_ARG;
   if (!prob->eta_code || !prob->eta_table || prob->n_codes < 1 || !st->z_pi) return PERT_E_ARG;
   if (prob->kind == PERT_KIND_STEP3 && !prob->rho_fixed) return PERT_E_ARG;

@@ -38,7 +38,7 @@ def assign_s_to_clones(s_phase_cells: pd.DataFrame, clone_df: pd.DataFrame, col_
         ok = (li >= 0) & np.isfinite(v)
         x = v[ok]
         Y = prof[li[ok]]
-        okc = np.isfinite(Y).all(axis=1)
+        okc = ~np.isnan(Y).any(axis=1)          # merged_df.dropna(): NaN rows only (inf stays)
         x, Y = x[okc], Y[okc]
         xc = x - x.mean()
         Yc = Y - Y.mean(0)

@@ -23,7 +23,8 @@ init_to_median(15) draws, 'median' = analytic medians), ``dirichlet_mode`` ('tor
 reproduces the reference's fp32 Dirichlet normaliser in the reported losses, 'exact' =
 fp64), ``tau_init_method`` ('batched' = all cells' GMM / threshold scan at once on the
 device, tau_init.py; 'sklearn' = the per-cell sklearn loop), ``n_jobs`` for the latter,
-and ``process_group`` (a torch.distributed group; default: the world when initialised).
+``process_group`` (a torch.distributed group; default: the world when initialised) and
+``log_steps`` (False: no per-step 'step: i, loss: ...' log lines).
 """
 from __future__ import annotations
 
@@ -45,6 +46,28 @@ from .sharding import cell_bounds, make_allreduce
 from .tau_init import guess_times_batched, prewarm_pool
 
 log = logging.getLogger("scdna_replication_tools_amd.pert_model")
+
+_REF_LOGGING = []
+
+
+def configure_reference_logging():
+    """The logging set-up the reference runs when pert_model is imported
+    (pert_model.py:25-33): root logger at DEBUG with basicConfig's stderr handler
+    (format '%(relativeCreated) 9d %(message)s') plus a stdout handler for DEBUG records,
+    so the per-step 'step: i, loss: ...' lines of every fit are visible.  Done once per
+    process; the drop-in module ``scdna_replication_tools.pert_model`` calls it at import,
+    as the reference does.  ``pert_infer_scRT(..., log_steps=False)`` silences the per-step
+    lines of a fit."""
+    if _REF_LOGGING:
+        return
+    import sys
+    logging.basicConfig(format='%(relativeCreated) 9d %(message)s', level=logging.DEBUG)
+    root = logging.getLogger()
+    h = logging.StreamHandler(sys.stdout)
+    h.setLevel(logging.DEBUG)
+    h.addFilter(lambda record: record.levelno <= logging.DEBUG)
+    root.addHandler(h)
+    _REF_LOGGING.append(h)
 
 
 def _converged(losses: List[float], i: int, min_iter: int, rel_tol: float) -> bool:
@@ -126,7 +149,7 @@ class pert_infer_scRT():
                  max_iter_step1=None, min_iter_step1=None, max_iter_step3=None, min_iter_step3=None,
                  cuda=False, seed=0, P=13, K=4, J=5, upsilon=6, run_step3=True, *, device=None,
                  init_method='sampled', dirichlet_mode='torch32', n_jobs=1, tau_init_method='batched',
-                 process_group=None):
+                 process_group=None, log_steps=True):
         self.cn_s = cn_s
         self.cn_g1 = cn_g1
         self.input_col = input_col
@@ -174,6 +197,7 @@ class pert_infer_scRT():
         # them in this process
         self.tau_pool_jobs = n_jobs if n_jobs > 1 else -1
         self.tau_init_method = tau_init_method
+        self.log_steps = log_steps
         self.timings = {}
         self.iters = {}
         self._inp = None
@@ -334,8 +358,9 @@ class pert_infer_scRT():
         """
         t0 = time.perf_counter()
         losses, reason = shard.run_svi(max_iter, min_iter, self.rel_tol)
-        for i, loss in enumerate(losses):
-            log.info('step: {}, loss: {}'.format(i, loss))
+        if self.log_steps and logging.getLogger().isEnabledFor(logging.INFO):
+            for i, loss in enumerate(losses):
+                logging.info('step: {}, loss: {}'.format(i, loss))      # root logger, as :747
         if reason == 1:
             print('ELBO converged at iteration ' + str(len(losses) - 1))
         elif reason == 2:
@@ -411,89 +436,92 @@ class pert_infer_scRT():
                 chr_col=self.chr_col, start_col=self.start_col, cn_state_col=self.cn_state_col, keys=keys_g)
             return prof, time.perf_counter() - t0
 
-        fut_prof = []
-        tic = time.perf_counter()
-        inp = self._prepare(on_g1_sorted=lambda t, k: fut_prof.append(helper.submit(on_device, consensus, t, k)))
-        if not fut_prof:                       # inputs prepared before this call: consensus now
-            fut_prof.append(helper.submit(on_device, consensus, self.cn_g1, inp.keys_g))
-        n_libs = self.L
-        self.timings["prep"] = time.perf_counter() - tic
-
-        def priors():
-            profiles, t_cons = fut_prof[0].result()         # ran earlier on this same thread
-            t0 = time.perf_counter()
-            etas = self._build_etas(inp, profiles)
-            t1 = time.perf_counter()
-            # step 2's tau initialisation (:790), its device part on a side stream
-            stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
-            with (torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()):
-                t_init, _, _ = self._guess_times(inp.reads_s, etas.argmax_states())
-                if stream is not None:
-                    stream.synchronize()
-            return profiles, etas, t_init, (t_cons + t1 - t0, time.perf_counter() - t1)
-
-        fut_priors = helper.submit(on_device, priors)
-
-        # ---- step 1: G1/2 cells doubled, cn / rep observed (:718-774)
-        st_g2, rd_g2, lb_g2, rep_g2 = prep.make_g1_g2_training_data(inp.states_g, inp.reads_g, inp.libs_g)
-        init1 = init_params(KIND_STEP1, rd_g2, lb_g2, n_libs, P, K, seed=self.seed, method=self.init_method)
-        s1 = self._shard(KIND_STEP1, dd, rd_g2, lb_g2, init1, cn_obs=st_g2, rep_obs=rep_g2)
-        logging.info('STEP 1: Learning reads to CN bias from low variance cells.')
-        losses_g = self._svi(s1, self.max_iter_step1, self.min_iter_step1, "step1")
-        c1 = s1.constrained()
-        lambda_fit = np.asarray(c1["expose_lambda"], dtype=np.float32)
-        beta_means_fit = np.asarray(c1["expose_beta_means"], dtype=np.float32)
-        del s1
-
-        # ---- step 2: S cells, enumerated (:776-830)
-        tic = time.perf_counter()
-        profiles, etas, t_init, (t_priors, t_guess) = fut_priors.result()
-        # wall time step 1 did not hide (the helper's own durations: timings["helper_*"])
-        self.timings["guess_times_s"] = time.perf_counter() - tic
-        self.timings["helper_priors"], self.timings["helper_guess_times_s"] = t_priors, t_guess
-        # (the helper runs its tasks in order: the two tau initialisers never share the pool)
-        fut_prep3 = helper.submit(on_device, self._prep_step3, inp, profiles) if self.run_step3 else None
-        ploidy = etas.argmax_states().astype(np.float32).mean(0)
-        init2 = init_params(KIND_STEP2, inp.reads_s, inp.libs_s, n_libs, P, K, ploidy=ploidy, t_init=t_init,
-                            beta_means=beta_means_fit, seed=self.seed, method=self.init_method)
-        s2 = self._shard(KIND_STEP2, dd, inp.reads_s, inp.libs_s, init2, eta=etas, lamb=float(lambda_fit[0]),
-                         beta_means=beta_means_fit)
-        logging.info('STEP 2: Jointly infer replication and CN states in high variance cells.')
-        losses_s = self._svi(s2, self.max_iter, self.min_iter, "step2")
-        tic = time.perf_counter()
-        cn_map, rep_map, c2 = self._decode(s2, dd)
-        trace_s = MapTrace(cn=cn_map, rep=rep_map, expose_u=c2["expose_u"], expose_rho=c2["expose_rho"],
-                           expose_a=c2["expose_a"], expose_tau=c2["expose_tau"])
-        cn_s_out, supp_s_out_df = self.package_s_output(
-            self.cn_s, trace_s, self._axes(inp.cells_s, inp.keys_s), lambda_fit, losses_g, losses_s)
-        self.timings["decode_package_s"] = time.perf_counter() - tic
-        rho_fit = c2["expose_rho"]
-        a_fit = c2["expose_a"]
-        del s2
-
-        cn_g1_out = supp_g1_out_df = None
-        if self.run_step3:
-            # ---- step 3: G1 cells with rho, a frozen (:834-896)
+        try:
+            fut_prof = []
             tic = time.perf_counter()
-            etas2, t_init2 = fut_prep3.result()
-            ploidy2 = etas2.argmax_states().astype(np.float32).mean(0)
-            self.timings["prep_step3"] = time.perf_counter() - tic      # the part step 2 did not hide
-            init3 = init_params(KIND_STEP3, inp.reads_g, inp.libs_g, n_libs, P, K, ploidy=ploidy2,
-                                t_init=t_init2, beta_means=beta_means_fit, seed=self.seed, method=self.init_method)
-            s3 = self._shard(KIND_STEP3, dd, inp.reads_g, inp.libs_g, init3, eta=etas2, lamb=float(lambda_fit[0]),
-                             beta_means=beta_means_fit, rho_fixed=np.asarray(rho_fit).reshape(-1),
-                             a_fixed=float(np.asarray(a_fit)[0]))
-            logging.info('STEP 3: Running pre-trained S-phase model on low variance cells.')
-            losses_s2 = self._svi(s3, self.max_iter_step3, self.min_iter_step3, "step3")
+            inp = self._prepare(on_g1_sorted=lambda t, k: fut_prof.append(helper.submit(on_device, consensus, t, k)))
+            if not fut_prof:                       # inputs prepared before this call: consensus now
+                fut_prof.append(helper.submit(on_device, consensus, self.cn_g1, inp.keys_g))
+            n_libs = self.L
+            self.timings["prep"] = time.perf_counter() - tic
+
+            def priors():
+                profiles, t_cons = fut_prof[0].result()         # ran earlier on this same thread
+                t0 = time.perf_counter()
+                etas = self._build_etas(inp, profiles)
+                t1 = time.perf_counter()
+                # step 2's tau initialisation (:790), its device part on a side stream
+                stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+                with (torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()):
+                    t_init, _, _ = self._guess_times(inp.reads_s, etas.argmax_states())
+                    if stream is not None:
+                        stream.synchronize()
+                return profiles, etas, t_init, (t_cons + t1 - t0, time.perf_counter() - t1)
+
+            fut_priors = helper.submit(on_device, priors)
+
+            # ---- step 1: G1/2 cells doubled, cn / rep observed (:718-774)
+            st_g2, rd_g2, lb_g2, rep_g2 = prep.make_g1_g2_training_data(inp.states_g, inp.reads_g, inp.libs_g)
+            init1 = init_params(KIND_STEP1, rd_g2, lb_g2, n_libs, P, K, seed=self.seed, method=self.init_method)
+            s1 = self._shard(KIND_STEP1, dd, rd_g2, lb_g2, init1, cn_obs=st_g2, rep_obs=rep_g2)
+            logging.info('STEP 1: Learning reads to CN bias from low variance cells.')
+            losses_g = self._svi(s1, self.max_iter_step1, self.min_iter_step1, "step1")
+            c1 = s1.constrained()
+            lambda_fit = np.asarray(c1["expose_lambda"], dtype=np.float32)
+            beta_means_fit = np.asarray(c1["expose_beta_means"], dtype=np.float32)
+            del s1
+
+            # ---- step 2: S cells, enumerated (:776-830)
             tic = time.perf_counter()
-            cn3, rep3, c3 = self._decode(s3, dd)
-            trace_s2 = MapTrace(cn=cn3, rep=rep3, expose_u=c3["expose_u"], expose_rho=rho_fit, expose_a=a_fit,
-                                expose_tau=c3["expose_tau"])
-            cn_g1_out, supp_g1_out_df = self.package_s_output(
-                self.cn_g1, trace_s2, self._axes(inp.cells_g, inp.keys_g), lambda_fit, losses_g, losses_s2)
-            self.timings["decode_package_g"] = time.perf_counter() - tic
-            del s3
-        helper.shutdown(wait=True)
+            profiles, etas, t_init, (t_priors, t_guess) = fut_priors.result()
+            # wall time step 1 did not hide (the helper's own durations: timings["helper_*"])
+            self.timings["guess_times_s"] = time.perf_counter() - tic
+            self.timings["helper_priors"], self.timings["helper_guess_times_s"] = t_priors, t_guess
+            # (the helper runs its tasks in order: the two tau initialisers never share the pool)
+            fut_prep3 = helper.submit(on_device, self._prep_step3, inp, profiles) if self.run_step3 else None
+            ploidy = etas.argmax_states().astype(np.float32).mean(0)
+            init2 = init_params(KIND_STEP2, inp.reads_s, inp.libs_s, n_libs, P, K, ploidy=ploidy, t_init=t_init,
+                                beta_means=beta_means_fit, seed=self.seed, method=self.init_method)
+            s2 = self._shard(KIND_STEP2, dd, inp.reads_s, inp.libs_s, init2, eta=etas, lamb=float(lambda_fit[0]),
+                             beta_means=beta_means_fit)
+            logging.info('STEP 2: Jointly infer replication and CN states in high variance cells.')
+            losses_s = self._svi(s2, self.max_iter, self.min_iter, "step2")
+            tic = time.perf_counter()
+            cn_map, rep_map, c2 = self._decode(s2, dd)
+            trace_s = MapTrace(cn=cn_map, rep=rep_map, expose_u=c2["expose_u"], expose_rho=c2["expose_rho"],
+                               expose_a=c2["expose_a"], expose_tau=c2["expose_tau"])
+            cn_s_out, supp_s_out_df = self.package_s_output(
+                self.cn_s, trace_s, self._axes(inp.cells_s, inp.keys_s), lambda_fit, losses_g, losses_s)
+            self.timings["decode_package_s"] = time.perf_counter() - tic
+            rho_fit = c2["expose_rho"]
+            a_fit = c2["expose_a"]
+            del s2
+
+            cn_g1_out = supp_g1_out_df = None
+            if self.run_step3:
+                # ---- step 3: G1 cells with rho, a frozen (:834-896)
+                tic = time.perf_counter()
+                etas2, t_init2 = fut_prep3.result()
+                ploidy2 = etas2.argmax_states().astype(np.float32).mean(0)
+                self.timings["prep_step3"] = time.perf_counter() - tic      # the part step 2 did not hide
+                init3 = init_params(KIND_STEP3, inp.reads_g, inp.libs_g, n_libs, P, K, ploidy=ploidy2,
+                                    t_init=t_init2, beta_means=beta_means_fit, seed=self.seed, method=self.init_method)
+                s3 = self._shard(KIND_STEP3, dd, inp.reads_g, inp.libs_g, init3, eta=etas2, lamb=float(lambda_fit[0]),
+                                 beta_means=beta_means_fit, rho_fixed=np.asarray(rho_fit).reshape(-1),
+                                 a_fixed=float(np.asarray(a_fit)[0]))
+                logging.info('STEP 3: Running pre-trained S-phase model on low variance cells.')
+                losses_s2 = self._svi(s3, self.max_iter_step3, self.min_iter_step3, "step3")
+                tic = time.perf_counter()
+                cn3, rep3, c3 = self._decode(s3, dd)
+                trace_s2 = MapTrace(cn=cn3, rep=rep3, expose_u=c3["expose_u"], expose_rho=rho_fit, expose_a=a_fit,
+                                    expose_tau=c3["expose_tau"])
+                cn_g1_out, supp_g1_out_df = self.package_s_output(
+                    self.cn_g1, trace_s2, self._axes(inp.cells_g, inp.keys_g), lambda_fit, losses_g, losses_s2)
+                self.timings["decode_package_g"] = time.perf_counter() - tic
+                del s3
+        finally:
+            # also when a fit or a helper task raised: no helper work outlives the call
+            helper.shutdown(wait=True, cancel_futures=True)
         self.timings["total"] = time.perf_counter() - t_all
         return cn_s_out, supp_s_out_df, cn_g1_out, supp_g1_out_df
 

@@ -62,7 +62,7 @@ def _run(kw, z, **extra):
     return losses, reason, cn.cpu().numpy(), rep.cpu().numpy(), sh.constrained()
 
 
-def _worker(rank, world, port, out_dir, variant):
+def _worker(rank, world, port, out_dir, variant, fused):
     from scdna_replication_tools_amd.sharding import make_allreduce, shard_slice
     from tests._problems import make_problem
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{}".format(port), rank=rank, world_size=world)
@@ -73,7 +73,7 @@ def _worker(rank, world, port, out_dir, variant):
         sl = shard_slice(N, world, rank)
         k2, z2 = _shard_inputs(kw, z, sl)
         losses, reason, cn, rep, c = _run(k2, z2, is_root=(rank == 0), n_cells_total=N, allreduce=make_allreduce(),
-                                          variant=variant)
+                                          variant=variant, fused=fused)
         torch.save({"losses": losses, "reason": reason, "cn": torch.as_tensor(cn), "rep": torch.as_tensor(rep),
                     "rho": torch.as_tensor(c["expose_rho"]), "tau": torch.as_tensor(c["expose_tau"])},
                    os.path.join(out_dir, "r{}.pt".format(rank)))
@@ -81,15 +81,18 @@ def _worker(rank, world, port, out_dir, variant):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("variant", [0, 3])      # 3: pert_enum_step + all-reduce + pert_adam_shared
-def test_two_ranks_match_single_rank(tmp_path, variant):
+# (variant, fused): the two-wave pass; the three-wave pass with separate launches (the
+# default); the one-launch step, sharded: pert_enum_step(update_shared=0) -> all-reduce of
+# the shared block -> pert_adam_shared
+@pytest.mark.parametrize("variant,fused", [(0, False), (3, False), (3, True)])
+def test_two_ranks_match_single_rank(tmp_path, variant, fused):
     from scdna_replication_tools_amd.sharding import shard_slice
     from tests._problems import make_problem
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), variant), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), variant, fused), nprocs=2, join=True)
     r = [torch.load(str(tmp_path / "r{}.pt".format(i)), weights_only=True) for i in range(2)]
     prob, kw, z = make_problem(KIND, seed=SEED)
     k1, z1 = _shard_inputs(kw, z, slice(None))
-    losses, reason, cn, rep, c = _run(k1, z1, variant=variant)
+    losses, reason, cn, rep, c = _run(k1, z1, variant=variant, fused=fused)
     assert r[0]["losses"] == r[1]["losses"]                  # one global trajectory on every rank
     assert r[0]["reason"] == r[1]["reason"] == reason
     assert len(r[0]["losses"]) == len(losses)                # same stopping iteration

@@ -41,7 +41,7 @@ CASES = [("step2", "clone", 13, 2), ("step2", "composite", 13, 2), ("step3", "cl
          ("step2", "clone", 13, 8), ("step1", "clone", 13, 8)]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3])
+@pytest.mark.parametrize("variant", [0, 3])
 @pytest.mark.parametrize("kind,prior,P,n_libs", CASES)
 def test_loss_and_grads_match_oracle(kind, prior, P, n_libs, variant):
     prob, kw, z = make_problem(kind, prior=prior, P=P, seed=3, n_libs=n_libs)
@@ -85,7 +85,7 @@ def test_torch32_loss_mode_reports_the_reference_fp32_constant(prior):
         np.testing.assert_array_equal(g32[name], g64[name])
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3])
+@pytest.mark.parametrize("variant", [0, 3])
 @pytest.mark.parametrize("kind", ["step2", "step3", "step1"])
 def test_adam_trajectory(kind, variant):
     """Three SVI steps: losses and every parameter after the updates."""
@@ -104,7 +104,7 @@ def test_adam_trajectory(kind, variant):
         np.testing.assert_allclose(pi_dev, c_ref["expose_pi"].numpy(), rtol=2e-3, atol=1e-6)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3])
+@pytest.mark.parametrize("variant", [0, 3])
 @pytest.mark.parametrize("kind", ["step2", "step3"])
 def test_decode_matches_oracle(kind, variant):
     prob, kw, z = make_problem(kind, seed=11)

@@ -7,6 +7,7 @@ restatements of their reference loops (pert_model.py:206-296).  The prior builde
 the correlation-matched methods are in tests/test_priors.py.
 """
 import inspect
+import os
 
 import numpy as np
 import pandas as pd
@@ -204,3 +205,46 @@ def test_import_paths_and_signatures_match_reference():
     for meth, params in ref_params.items():
         assert [p for p in inspect.signature(getattr(pert_infer_scRT, meth)).parameters if p != "self"] == params
     assert inspect.signature(pert_infer_scRT.build_composite_cn_prior).parameters["weight"].default == 1e5
+
+
+def test_reference_logging_and_per_step_lines(capsys):
+    """Importing the drop-in pert_model configures root logging as the reference's import
+    does (pert_model.py:25-33), and every fit logs 'step: i, loss: ...' on the root logger
+    (:747, :805, :872); log_steps=False silences them."""
+    import logging
+    import subprocess
+    import sys
+    out = subprocess.run([sys.executable, "-c", "import logging, scdna_replication_tools.pert_model; "
+                          "r = logging.getLogger(); print(r.level, len(r.handlers))"],
+                         capture_output=True, text=True, check=True, cwd=os.path.dirname(os.path.dirname(__file__)))
+    assert out.stdout.split() == ["10", "2"]                 # DEBUG; basicConfig's + the stdout handler
+    root = logging.getLogger()
+    m, s, g = _model(seed=2)
+
+    class FakeShard:
+        def run_svi(self, max_iter, min_iter, rel_tol):
+            return [3.0, 2.5, 2.25], 1
+
+    class Catch(logging.Handler):
+        def __init__(self):
+            super().__init__()
+            self.msgs = []
+
+        def emit(self, record):
+            self.msgs.append(record.getMessage())
+
+    h = Catch()
+    root.addHandler(h)
+    level = root.level
+    root.setLevel(logging.INFO)
+    try:
+        m._svi(FakeShard(), 10, 1, "step2")
+        assert h.msgs == ["step: 0, loss: 3.0", "step: 1, loss: 2.5", "step: 2, loss: 2.25"]
+        assert "ELBO converged at iteration 2" in capsys.readouterr().out
+        h.msgs.clear()
+        m.log_steps = False
+        m._svi(FakeShard(), 10, 1, "step2")
+        assert h.msgs == []
+    finally:
+        root.removeHandler(h)
+        root.setLevel(level)

@@ -22,7 +22,8 @@ Extra keyword arguments (all optional): ``device`` (default ``cuda``, or
 init_to_median(15) draws, 'median' = analytic medians), ``dirichlet_mode`` ('torch32'
 reproduces the reference's fp32 Dirichlet normaliser in the reported losses, 'exact' =
 fp64), ``tau_init_method`` ('batched' = all cells' GMM / threshold scan at once on the
-device, tau_init.py; 'sklearn' = the per-cell sklearn loop), ``n_jobs`` for the latter,
+device plus the exact host path for the cells rounding could change, tau_init.py;
+'sklearn' = the per-cell sklearn loop), ``n_jobs`` (threads of either; no worker processes),
 ``process_group`` (a torch.distributed group; default: the world when initialised) and
 ``log_steps`` (False: no per-step 'step: i, loss: ...' log lines).
 """
@@ -43,7 +44,7 @@ from ._native import KIND_STEP1, KIND_STEP2, KIND_STEP3
 from .engine import EtaCodebook, PertShard
 from .init import init_params
 from .sharding import cell_bounds, make_allreduce
-from .tau_init import guess_times_batched, prewarm_pool
+from .tau_init import default_threads, guess_times_batched
 
 log = logging.getLogger("scdna_replication_tools_amd.pert_model")
 
@@ -192,10 +193,9 @@ class pert_infer_scRT():
         self.init_method = init_method
         self.dirichlet_mode = dirichlet_mode
         self.n_jobs = n_jobs
-        # worker processes of the batched tau initialiser's per-cell path (its fragile cells):
-        # the affinity cores (at most 16) unless n_jobs > 1 names a count; tau_pool_jobs=1 runs
-        # them in this process
-        self.tau_pool_jobs = n_jobs if n_jobs > 1 else -1
+        # threads of the tau initialiser's exact host path (no worker processes): the affinity
+        # cores (at most 16) unless n_jobs > 1 names a count
+        self.tau_threads = n_jobs if n_jobs > 1 else default_threads()
         self.tau_init_method = tau_init_method
         self.log_steps = log_steps
         self.timings = {}
@@ -321,7 +321,7 @@ class pert_infer_scRT():
     def _guess_times(self, reads, cn_states):
         if self.tau_init_method == 'sklearn':
             return prep.guess_times(reads, cn_states, self.upsilon, self.n_jobs)
-        return guess_times_batched(reads, cn_states, self.upsilon, device=self.device, n_jobs=self.tau_pool_jobs)
+        return guess_times_batched(reads, cn_states, self.upsilon, device=self.device, n_threads=self.tau_threads)
 
     def make_gc_features(self, x):
         """pert_model.py:460-463: columns [x^K, ..., x, 1]."""
@@ -408,13 +408,6 @@ class pert_infer_scRT():
         dd = _Dist(self._group)
         if self.device.type == "cuda" and self.device.index is not None:
             torch.cuda.set_device(self.device)
-        if dd.world > 1 and self.n_jobs <= 1:
-            # every rank runs the tau initialiser on all cells; worker processes started from a
-            # rank (whose __main__ may be a launcher's) are not safe to assume -- in-process
-            self.tau_pool_jobs = 1
-        if self.tau_init_method != 'sklearn' and self._long_rows() >= 10 ** 7:
-            # genome-scale inputs: start the per-cell worker pool now, overlapping prep and step 1
-            prewarm_pool(self.tau_pool_jobs)           # (no-op for 1)
         # host work that only steps 2/3 need runs on a helper thread: the consensus profiles as
         # soon as the G1/2 table is sorted (while the S table is prepared), the step-2 prior and
         # tau initialisation while step 1 fits, then (during step 2) the step-3 prior and tau

@@ -19,6 +19,8 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import List, Optional
 
+import os
+
 import numpy as np
 import pandas as pd
 
@@ -849,8 +851,11 @@ def guess_times(reads: np.ndarray, cn_states: np.ndarray, upsilon: float = 6, n_
     norm = (x / torch.where(st > 0.0, st, half)).numpy()
     cols = [norm[:, i].reshape(-1, 1) for i in range(norm.shape[1])]
     if n_jobs != 1:
-        from joblib import Parallel, delayed
-        fr = Parallel(n_jobs=n_jobs)(delayed(manhattan_binarization)(c) for c in cols)
+        # threads of this process (no worker processes); -1: the affinity cores, at most 16
+        from concurrent.futures import ThreadPoolExecutor
+        nt = n_jobs if n_jobs > 0 else max(1, min(16, len(os.sched_getaffinity(0))))
+        with ThreadPoolExecutor(max_workers=nt) as ex:
+            fr = list(ex.map(manhattan_binarization, cols))
     else:
         fr = [manhattan_binarization(c) for c in cols]
     t_init = np.array([f[1] for f in fr], dtype=np.float32)

@@ -1,40 +1,39 @@
 """Batched ``guess_times`` (reference pert_model.py:364-457): the per-cell S-phase time
-guess t_init, for every cell at once on the fit's device.
+guess t_init, for every cell, equal to the reference's per-cell result.
 
 The reference loops over cells in Python and, per cell, standardises the
 CN-normalised read profile, fits ``sklearn.mixture.GaussianMixture(n_components=2,
 random_state=0)`` (k-means++ / Lloyd initialisation, then EM), picks two binary
 levels from the GMM means (or from percentiles chosen by the skew when the means are
 closer than 0.7), scans 100 thresholds for the smallest Manhattan distance between
-the profile and its binarisation, and returns the replicated fraction.  Here every
-stage runs as one batched tensor program over the (L, N) matrix with a per-cell
-"still iterating" mask, following the same algorithm and stopping rules:
+the profile and its binarisation, and returns the replicated fraction -- all in fp32.
 
-* k-means++ (sklearn cluster/_kmeans.py ``_kmeans_plusplus``) with the RandomState(0)
-  draws sklearn makes - the first-centre ``choice`` and the two local-trial
-  ``uniform`` values do not depend on the data, so they are drawn once on the host
-  with the same generator and shared by every cell;
-* Lloyd iterations (``_kmeans_single_lloyd``: max 300, strict-label or
-  centre-shift <= 1e-4 * var convergence, final re-assignment);
-* EM of a 2-component 1-D Gaussian mixture (``BaseMixture.fit_predict``: max 100,
-  |delta mean log-likelihood| < 1e-3, reg_covar 1e-6, 10 eps on the counts);
-* skew (scipy ``skew``, biased), linear percentiles, the 100-threshold scan with
-  first-minimum ties.
+Two passes:
 
-Arithmetic is fp64 while sklearn fits the profile in its own fp32 arithmetic, and read
-counts are integers, so standardised profiles hold many identical values: a group of
-them lying on a k-means decision boundary, an EM lower-bound change at the 1e-3
-tolerance, a mean gap or skew at its threshold, or a near-tie in the threshold scan
-can make the two arithmetics take different branches.  Every such decision is checked
-against a margin (``FRAGILE``, relative) and the cells where any of them falls inside
-it ("fragile" cells) are recomputed with the reference's per-cell sklearn path
-(prep.manhattan_binarization).  Up to ``MINOR_EXACT_MAX_L`` (2,000) bins that covers every
-flagged cell (a few %), so the result is the reference's for every cell.  At genome scale
-(5,451 bins) the finer near-ties -- a k-means++ draw next to a cumulative-sum boundary, a
-threshold scan whose minimum is flat against fp32 summation noise, points within the
-levels' rounding budget of the threshold -- flag about half the cells and each per-cell fit
-takes about a second, so only the branch decisions are recomputed there and the
-near-tie cells keep the batched value.  tests/test_tau_init.py pins both regimes.
+* **Batched, fp64, on the fit's device** (``binarization_fraction``): every stage as one
+  tensor program over the (L, N) matrix with a per-cell "still iterating" mask --
+  k-means++ (sklearn cluster/_kmeans.py ``_kmeans_plusplus``, with the RandomState(0)
+  draws sklearn makes, which do not depend on the data), Lloyd (``_kmeans_single_lloyd``:
+  max 300, strict-label or centre-shift convergence, final re-assignment), EM of a
+  2-component 1-D mixture (``BaseMixture.fit_predict``: max 100, |delta lower bound| <
+  1e-3), skew, percentiles, the threshold scan.  Each decision fp32 rounding could flip
+  is checked against a margin: the k-means partition (ties of identical read values on
+  a decision, a k-means++ draw next to a cumulative-sum boundary, the Lloyd / EM
+  stopping rules, the mean-gap and skew thresholds, the two tie-direction runs
+  disagreeing) and the scan (a minimum flat against fp32 summation noise, points within
+  the levels' rounding budget of the chosen threshold).  A cell none of them flags
+  keeps this pass's result.
+* **Exact, on the host** (``exact_fractions``) for the flagged cells (a few % up to
+  ~2,000 bins, about half at 5,451): the reference's fp32 arithmetic restated call for
+  call -- the per-cell standardisation, sklearn's own k-means functions where the
+  partition was uncertain (the batched labels otherwise), sklearn's EM op for op with
+  the same per-cell BLAS calls, and the scan with the candidate thresholds summed in
+  fp32 exactly as ``cityblock`` sums them -- batched over cells where numpy gives the
+  same bits, on threads of this process (no worker processes).
+
+So every cell's t_init is bit-identical to the reference's per-cell path
+(prep.guess_times) on the same machine; tests/test_tau_init.py checks each stage of the
+exact path against sklearn and the whole against prep.guess_times, up to 5,451 bins.
 """
 from __future__ import annotations
 
@@ -62,8 +61,10 @@ EPS32 = float(np.finfo(np.float32).eps)
 
 
 def _level_margin(L: int) -> float:
-    """Relative rounding budget of the scan levels b0, b1 (see above)."""
-    return 6e-7 * float(np.sqrt(L))
+    """Relative rounding budget of the scan levels b0, b1: sklearn's fp32 EM means differ
+    from the fp64 ones by up to 4e-7 sqrt(L) of max |mean| (measured against the exact
+    restatement, exact_gmm_means, at 271 and 5,451 bins); 2.5x that."""
+    return 1e-6 * float(np.sqrt(L))
 
 
 def _rng_draws(n: int):
@@ -76,9 +77,11 @@ def _rng_draws(n: int):
     return first, u
 
 
-def _kmeans_pp(X: torch.Tensor, first: int, u: np.ndarray, fragile: torch.Tensor = None) -> torch.Tensor:
+def _kmeans_pp(X: torch.Tensor, first: int, u: np.ndarray, fragile: torch.Tensor = None, alts: list = None):
     """k-means++ for 2 centres, batched over the columns of X (L, N) -> (2, N).  Marks in
-    ``fragile`` the columns whose candidate draw or choice is within the rounding margin."""
+    ``fragile`` the columns whose candidate draw or choice is within the rounding margin
+    and appends to ``alts`` the (N, 6) second centres the reference could have drawn there
+    (either trial's candidate and its neighbours on the cumulative sum)."""
     L, N = X.shape
     c0 = X[first]                                                    # (N,)
     d0 = (X - c0) ** 2                                               # closest_dist_sq (L, N)
@@ -98,6 +101,9 @@ def _kmeans_pp(X: torch.Tensor, first: int, u: np.ndarray, fragile: torch.Tensor
         fragile |= near.any(1)
         differ = (xc[:, 0] != xc[:, 1]) & ((pots[0] - pots[1]).abs() <= PP_MARGIN * pots.abs().max(0).values)
         fragile |= differ
+        if alts is not None:
+            nb = torch.cat([(cand - 1).clamp(min=0), cand, (cand + 1).clamp(max=L - 1)], dim=1)   # (N, 6)
+            alts.append(torch.gather(X.T, 1, nb))
     return torch.stack([c0, c1])
 
 
@@ -209,20 +215,22 @@ def binarization_fraction(Xraw: torch.Tensor, return_fragile: bool = False, retu
     returns the replicated fraction per column (and, with ``return_fragile``, the mask of
     the columns whose outcome fp32 rounding could change, see the module doc): the
     pipeline runs twice, with ties on a k-means decision broken towards either centre,
-    and a column whose two results differ is fragile too.  ``return_minor`` splits the
-    mask in two: branch decisions (Lloyd / EM stopping, mean-gap and skew thresholds, the
-    tie-direction runs disagreeing) and near-ties of finer grain (the k-means++ candidate
-    draw, a flat minimum of the threshold scan, points within the levels' rounding budget of
-    the chosen threshold)."""
+    and a column whose two results (fraction or k-means labels) differ is fragile too.
+    ``return_minor`` splits the mask in two -- ``labels``: the k-means partition is not
+    certain (Lloyd / EM stopping, mean-gap and skew thresholds, the tie-direction runs
+    disagreeing, a k-means++ candidate draw next to a cumulative-sum boundary), and
+    ``near``: the partition is certain but the levels' fp32 rounding could move the scan
+    (a flat minimum, points within the levels' rounding budget of the chosen threshold) --
+    and also returns the (L, N) k-means labels (True = centre 1)."""
     if not return_fragile:
         return _binarize(Xraw, 0.0)[0]
-    f_hi, fr_hi, pp_hi, sc_hi, mn_hi = _binarize(Xraw, TIE, with_minor=True)
-    f_lo, fr_lo, pp_lo, sc_lo, mn_lo = _binarize(Xraw, -TIE, with_minor=True)
-    decisions = fr_hi | fr_lo | (f_hi != f_lo)
-    near = pp_hi | pp_lo | sc_hi | sc_lo | (mn_hi > 0) | (mn_lo > 0)
+    f_hi, fr_hi, pp_hi, sc_hi, mn_hi, lab_hi = _binarize(Xraw, TIE, with_minor=True)
+    f_lo, fr_lo, pp_lo, sc_lo, mn_lo, lab_lo = _binarize(Xraw, -TIE, with_minor=True)
+    labels = fr_hi | fr_lo | (f_hi != f_lo) | pp_hi | pp_lo | (lab_hi != lab_lo).any(0)
+    near = sc_hi | sc_lo | (mn_hi > 0) | (mn_lo > 0)
     if return_minor:
-        return f_hi, decisions, near
-    return f_hi, decisions | near
+        return f_hi, labels, near, lab_hi
+    return f_hi, labels | near
 
 
 def _binarize(Xraw: torch.Tensor, tie_bias: float, with_minor: bool = False):
@@ -235,7 +243,20 @@ def _binarize(Xraw: torch.Tensor, tie_bias: float, with_minor: bool = False):
     fragile = torch.zeros(N, dtype=torch.bool, device=X.device)
     frag_pp = torch.zeros(N, dtype=torch.bool, device=X.device)
     frag_scan = torch.zeros(N, dtype=torch.bool, device=X.device)
-    lab1 = _lloyd(Xc, _kmeans_pp(Xc, first, u, frag_pp), tol, fragile=fragile, tie_bias=tie_bias)
+    alts = []
+    cen = _kmeans_pp(Xc, first, u, frag_pp, alts)
+    lab1 = _lloyd(Xc, cen, tol, fragile=fragile, tie_bias=tie_bias)
+    if bool(frag_pp.any()):
+        # a k-means++ draw within rounding of a boundary: the partition is still certain when
+        # Lloyd ends in the same labels from every second centre the reference could have drawn
+        idx = torch.nonzero(frag_pp)[:, 0]
+        same = torch.ones(idx.numel(), dtype=torch.bool, device=X.device)
+        for a in range(alts[0].shape[1]):
+            fr_a = torch.zeros(idx.numel(), dtype=torch.bool, device=X.device)
+            lab_a = _lloyd(Xc[:, idx], torch.stack([cen[0, idx], alts[0][idx, a]]), tol[idx], fragile=fr_a,
+                           tie_bias=tie_bias)
+            same &= (lab_a == lab1[:, idx]).all(0) & ~fr_a
+        frag_pp[idx[same]] = False
     mu = _gmm_means(X, lab1, fragile=fragile)
     gap = (mu[0] - mu[1]).abs()
     b0, b1 = torch.minimum(mu[0], mu[1]), torch.maximum(mu[0], mu[1])
@@ -281,93 +302,304 @@ def _binarize(Xraw: torch.Tensor, tie_bias: float, with_minor: bool = False):
         span = (b1 - b0)[s:s + chunk].abs()
         near = ((xs[None] - t[:, None, :]).abs() <= 2 * db[None, None] + 1e-6).sum(1).to(d.dtype)   # (100, n)
         near_best = near.gather(0, bi[None])
-        slack = (2 * dcnt * db[None] + (near + near_best) * span[None]
-                 + 4 * EPS32 * (np.log2(max(L, 2)) + 2) * dmin)
+        # fp32 summation: the reference's d(t) and d(t') are pairwise sums of the same terms
+        # except at the dcnt points t and t' binarise differently, so every partial sum of the
+        # tree away from those points is bitwise the same in both and cancels; what remains is
+        # the rounding along the paths from those points to the root -- at most u |partial|
+        # per node: <= (16 + 16 + 3 x 8) x 16 terms of the point's leaf block (numpy's 8
+        # accumulators of <= 16 terms, three combining levels) and d / 2^h at tree level h
+        # (min(2^h, dcnt) such nodes) -- in each of the two sums.
+        tmax = torch.maximum((xs - b0[None, s:s + chunk]).abs(), (xs - b1[None, s:s + chunk]).abs()).amax(0)
+        noise = EPS32 * (dcnt * 56 * 16 * tmax[None] + (torch.log2(dcnt + 1) + 2) * dmin)
+        # a point x within 2 db of a threshold may sit on its other side in the reference: that
+        # moves d by |x - b1| - |x - b0| = b0 + b1 - 2x (x between the levels), i.e. by at most
+        # |b0 + b1 - 2t| + 4 db -- small near the scan's optimum, the levels' midpoint
+        mid = (b0 + b1)[None, s:s + chunk]
+        flip = (mid - 2 * t).abs() + 4 * db[None]
+        slack = 2 * dcnt * db[None] + near * flip + near_best * flip.gather(0, bi[None]) + noise
         frag_scan[s:s + chunk] |= (((dcnt > 0) | (near > 0)) & (d - dmin <= slack)).any(0)
         minor[s:s + chunk] = near_best[0]
     frac = (X > best[None, :]).sum(0).to(torch.float64) / L
     if with_minor:
-        return frac, fragile, frag_pp, frag_scan, minor
+        return frac, fragile, frag_pp, frag_scan, minor, lab1
     return frac, fragile | frag_pp | frag_scan | (minor > 0)
 
 
-def _pool_size(n_jobs: int) -> int:
-    return n_jobs if n_jobs > 0 else min(16, len(os.sched_getaffinity(0)))
+# ------------------------------------------------------------------------------------------
+# The exact host path: the reference's per-cell fp32 arithmetic, restated call for call and
+# batched over cells where numpy gives the same bits (elementwise ufuncs, per-row reductions),
+# with the same BLAS calls per cell as sklearn makes.  tests/test_tau_init.py checks every
+# stage against sklearn / the per-cell reference bit for bit.
+F32 = np.float32
+_LOG2PI32 = np.log(2 * np.pi).astype(np.float32)        # _estimate_log_gaussian_prob's constant
+_EPS10 = 10 * np.finfo(np.float32).eps                   # _estimate_gaussian_parameters' nk guard
+_NEG_INF = F32(-np.inf)
+SCAN_SLACK = 1e-4   # relative: fp64 scan values within this of the minimum are re-summed in fp32
 
 
-_WARM = {}
+def standardize_rows(norm_rows: np.ndarray) -> np.ndarray:
+    """``(X - np.mean(X)) / np.std(X)`` (pert_model.py:367) for every row of an (n, L) fp32
+    array: numpy's per-row reductions are the 1-D ones (pairwise sums), so each row equals
+    the reference's per-cell result."""
+    X = np.ascontiguousarray(norm_rows, dtype=F32)
+    return (X - np.mean(X, axis=1, keepdims=True)) / np.std(X, axis=1, keepdims=True)
 
 
-def _warm_worker():
-    import sklearn.mixture  # noqa: F401  (the per-cell path's import, done once per worker)
-    return 0
+def _sq_dist_upcast(c: np.ndarray, X: np.ndarray) -> np.ndarray:
+    """sklearn metrics/pairwise.py ``_euclidean_distances(c, X, Y_norm_squared=<fp32>,
+    squared=True)`` for fp32 data with one feature: ``_euclidean_distances_upcast`` forms
+    -2 c x + c^2 + x^2 in float64 (the product and squares are exact there), casts to
+    float32 and clips at 0.  (k, 1), (L, 1) -> (k, L) float32."""
+    c64 = c.astype(np.float64)
+    x64 = X.astype(np.float64)
+    d = -2 * (c64 @ x64.T)
+    d += c64 * c64
+    d += (x64 * x64).T
+    out = d.astype(np.float32)
+    np.maximum(out, 0, out=out)
+    return out
 
 
-def prewarm_pool(n_jobs: int = -1):
-    """Start the joblib (loky) worker processes of the per-cell path in a background thread,
-    so their start-up (a few seconds: interpreter + sklearn import per worker) overlaps the
-    host prep and the first fits instead of delaying guess_times; guess_times_batched waits
-    for it and reuses the same executor."""
-    import threading
-    nj = _pool_size(n_jobs)
-    if nj <= 1 or nj in _WARM:
-        return
+def exact_kmeans_labels(x: np.ndarray) -> np.ndarray:
+    """The labels of ``cluster.KMeans(n_clusters=2, n_init=1, random_state=RandomState(0))
+    .fit(X)`` as GaussianMixture's k-means initialisation runs it (sklearn
+    mixture/_base.py _initialize_parameters; cluster/_kmeans.py KMeans.fit): tolerance from
+    the uncentred data, centring by the fp32 mean, k-means++ (``_kmeans_plusplus`` restated
+    with the same RandomState draws, distances and BLAS products), then sklearn's own Lloyd
+    (``_kmeans_single_lloyd``, on one OpenMP thread: the reference's thread count only
+    changes the last bits of the centre sums, never a label short of an exact tie)."""
+    from sklearn.cluster._kmeans import _kmeans_single_lloyd, _tolerance
+    X = np.array(x, dtype=F32, order="C").reshape(-1, 1)
+    n = X.shape[0]
+    tol = _tolerance(X, 1e-4)
+    rs = np.random.RandomState(0)
+    sw = np.ones(n, dtype=X.dtype)
+    X -= X.mean(axis=0)
+    centers = np.empty((2, 1), dtype=X.dtype)
+    centers[0] = X[rs.choice(n, p=sw / sw.sum())]
+    closest = _sq_dist_upcast(centers[0, np.newaxis], X)
+    pot = closest @ sw
+    rand_vals = rs.uniform(size=2 + int(np.log(2))) * pot
+    cand = np.searchsorted(np.cumsum(sw * closest, dtype=np.float64), rand_vals)
+    np.clip(cand, None, closest.size - 1, out=cand)
+    dc = _sq_dist_upcast(X[cand], X)
+    np.minimum(closest, dc, out=dc)
+    centers[1] = X[cand[np.argmin(dc @ sw.reshape(-1, 1))]]
+    labels, _, _, _ = _kmeans_single_lloyd(X, sw, centers, max_iter=300, verbose=False, tol=tol, n_threads=1)
+    return labels.astype(np.int8)
 
-    def run():
-        from joblib import Parallel, delayed
-        Parallel(n_jobs=nj)(delayed(_warm_worker)() for _ in range(nj))
 
-    th = threading.Thread(target=run, name="pert-tau-pool", daemon=True)
-    _WARM[nj] = th
-    th.start()
+def _lse2(a: np.ndarray) -> np.ndarray:
+    """scipy.special.logsumexp(a, axis=-1) of an (..., 2) fp32 array, op for op as scipy's
+    _logsumexp (b=None); its two-element reductions written as the equal elementwise ops."""
+    a0, a1 = a[..., 0], a[..., 1]
+    a_max = np.maximum(a0, a1)
+    i0, i1 = a0 == a_max, a1 == a_max
+    m = i0.astype(F32) + i1.astype(F32)
+    shift = np.where(np.isfinite(a_max), a_max, F32(0))
+    am = np.empty_like(a)
+    am[..., 0] = np.where(i0, _NEG_INF, a0)
+    am[..., 1] = np.where(i1, _NEG_INF, a1)
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore", under="ignore"):
+        e = np.exp(am - shift[..., None])
+        s = e[..., 0] + e[..., 1]
+        s = np.where(s == 0, s, s / m)
+        sgn = np.sign(s + 1) * np.sign(m)
+        s = np.where(s < -1, -s - 2, s)
+        out = np.log1p(s) + np.log(np.abs(m)) + a_max
+    out[sgn < 0] = np.nan
+    return out
 
 
-def _pool_state(n_jobs: int) -> str:
-    """'none' (no background start), 'warming' or 'ready' -- without waiting."""
-    th = _WARM.get(_pool_size(n_jobs))
-    if th is None:
-        return "none"
-    return "warming" if th.is_alive() else "ready"
+def _distinct(Xs: np.ndarray):
+    """Per row of Xs (n, L): the sorted distinct values, their counts and the inverse map."""
+    n, L = Xs.shape
+    uniq, counts, inv = [], [], np.empty((n, L), np.intp)
+    for i in range(n):
+        u, iv, c = np.unique(Xs[i], return_inverse=True, return_counts=True)
+        uniq.append(u)
+        counts.append(c)
+        inv[i] = iv
+    return uniq, counts, inv
+
+
+def exact_gmm_means(Xs: np.ndarray, labels: np.ndarray, max_iter: int = 100, tol: float = 1e-3,
+                    distinct=None) -> np.ndarray:
+    """``GaussianMixture(n_components=2, random_state=0).fit_predict(X).means_`` for every
+    row X of Xs (n, L) fp32, from the k-means ``labels`` (n, L): sklearn's EM
+    (mixture/_base.py fit_predict; _gaussian_mixture.py _initialize, _m_step,
+    _estimate_gaussian_parameters, _estimate_log_gaussian_prob with 'full' covariances, one
+    feature) restated op for op.  The E step is elementwise in x, so it runs on each row's
+    distinct values and is gathered back.  The M step's sums are the reference's own:
+    ``resp.sum(axis=0)`` (numpy adds the rows in order, i.e. a cumulative sum), and per cell
+    the BLAS calls sklearn makes -- ``np.dot(resp.T, X)`` (gemv on an (L, 2) C-ordered
+    array) and ``np.dot(resp[:, k] * diff.T, diff)`` (sdot of two contiguous vectors); the
+    1x1 Cholesky factor and triangular solve are sqrt and 1 / l.  Returns (n, 2) fp32."""
+    n, L = Xs.shape
+    xs = [np.array(Xs[i], dtype=F32).reshape(L, 1) for i in range(n)]
+    uniq, _, inv = _distinct(Xs) if distinct is None else distinct
+    U = max(len(u) for u in uniq)
+    Xu = np.empty((n, U), F32)
+    for i, u in enumerate(uniq):
+        Xu[i, :len(u)] = u
+        Xu[i, len(u):] = u[0]
+    resp = np.zeros((n, L, 2), dtype=F32)
+    resp[np.arange(n)[:, None], np.arange(L)[None, :], np.asarray(labels, np.intp)] = 1
+
+    def mstep(resp, rows):
+        m = len(rows)
+        nk = np.cumsum(resp, axis=1)[:, -1, :] + _EPS10                  # (m, 2)
+        dots = np.empty((m, 2), F32)
+        for j, i in enumerate(rows):
+            dots[j] = np.dot(resp[j].copy().T, xs[i])[:, 0]
+        means = dots / nk
+        diff = Xs[rows][:, None, :] - means[:, :, None]                   # (m, 2, L): X - means[k]
+        prod = resp.transpose(0, 2, 1) * diff                             # resp[:, k] * diff.T
+        cov = np.empty((m, 2), F32)
+        for j in range(m):
+            cov[j, 0] = np.dot(prod[j, 0], diff[j, 0])
+            cov[j, 1] = np.dot(prod[j, 1], diff[j, 1])
+        return nk, means, cov / nk + 1e-6
+
+    w, means, cov = mstep(resp, np.arange(n))
+    w = w / L
+    pc = F32(1) / np.sqrt(cov)
+    lower = np.full(n, -np.inf, dtype=F32)
+    active = np.ones(n, bool)
+    for _ in range(max_iter):
+        a = np.flatnonzero(active)
+        pa = pc[a]
+        y = Xu[a][:, :, None] * pa[:, None, :] - (means[a] * pa)[:, None, :]
+        wlp = (-0.5 * (1 * _LOG2PI32 + np.square(y)) + np.log(pa)[:, None, :]) + np.log(w[a])[:, None, :]
+        lpn_u = _lse2(wlp)
+        with np.errstate(under="ignore"):
+            resp_u = np.exp(wlp - lpn_u[:, :, None])
+        ia = inv[a] + (np.arange(len(a)) * U)[:, None]       # flat gather of the distinct values
+        lb = np.mean(np.take(lpn_u, ia), axis=1)
+        ia2 = 2 * ia
+        w2, m2, c2 = mstep(np.take(resp_u, np.stack([ia2, ia2 + 1], axis=2)), a)
+        w[a] = w2 / (w2[:, :1] + w2[:, 1:])
+        means[a], cov[a] = m2, c2
+        pc[a] = F32(1) / np.sqrt(c2)
+        change = lb - lower[a]
+        lower[a] = lb
+        active[a[np.abs(change) < tol]] = False
+        if not active.any():
+            break
+    return means
+
+
+def exact_scan(x: np.ndarray, mean_0, mean_1, MEAN_GAP=MEAN_GAP_THRESH, EARLY=EARLY_S_SKEW_THRESH,
+               LATE=LATE_S_SKEW_THRESH, distinct=None) -> float:
+    """pert_model.py:377-423 for one standardized fp32 profile x (L,) and the GMM means:
+    the levels (means, or percentiles chosen by the skew), ``np.linspace(b0, b1, 100)``
+    thresholds and the first threshold of least ``cityblock(X, B)``; returns the replicated
+    fraction.  The 100 distances are evaluated in fp64 from sorted prefix sums; only the
+    thresholds within SCAN_SLACK of the least are summed the reference's way (fp32
+    ``abs(X - B).sum()``; its error is < 1e-5 of the sum), which decides among them."""
+    from scipy.stats import skew
+    X = np.asarray(x, dtype=F32).reshape(-1)
+    L = X.size
+    mean_gap = abs(mean_0 - mean_1)
+    b0, b1 = min(mean_0, mean_1), max(mean_0, mean_1)
+    if mean_gap < MEAN_GAP:
+        cs = skew(X)
+        if cs > EARLY:
+            b0, b1 = np.percentile(X, 50), np.percentile(X, 95)
+        elif cs < LATE:
+            b0, b1 = np.percentile(X, 5), np.percentile(X, 50)
+        else:
+            b0, b1 = np.percentile(X, 25), np.percentile(X, 75)
+    th = np.linspace(b0, b1, 100)
+    u, c = np.unique(X, return_counts=True) if distinct is None else distinct
+    u64 = u.astype(np.float64)
+    C = np.concatenate([[0], np.cumsum(c)])                  # points among the first j distinct values
+    S = np.concatenate([[0.0], np.cumsum(c * u64)])
+    nu = len(u64)
+    k = np.searchsorted(u64, th.astype(np.float64), side="right")     # x <= t: B = b0 there
+
+    def absdev(lo, hi, level):
+        # sum of |x - level| over the distinct-value ranges [lo, hi), split at the level
+        m = np.minimum(np.maximum(np.searchsorted(u64, level, side="right"), lo), hi)
+        return ((C[m] - C[lo]) * level - (S[m] - S[lo])) + ((S[hi] - S[m]) - (C[hi] - C[m]) * level)
+
+    d = absdev(np.zeros_like(k), k, float(b0)) + absdev(k, np.full_like(k, nu), float(b1))
+    cand = np.flatnonzero(d <= d.min() * (1 + SCAN_SLACK) + 1e-9)
+    best, lowest = None, np.inf
+    for i in cand:                                            # in threshold order, strict '<'
+        dist = np.abs(X - np.where(X > th[i], b1, b0)).sum()
+        if dist < lowest:
+            lowest, best = dist, th[i]
+    cell_rt = np.where(X > best, 1, 0)
+    return cell_rt.sum() / len(cell_rt)
+
+
+def exact_fractions(norm_cols: np.ndarray, labels=None, n_threads: int = 1, chunk: int = 32) -> np.ndarray:
+    """The reference's replicated fraction (manhattan_binarization, pert_model.py:364-423)
+    of every column of ``norm_cols`` (L, n) fp32 (the CN-normalised reads), bit for bit:
+    standardisation, k-means labels (``labels`` (n, L) where the batched pass has settled
+    them, rows of -1 to compute them here), GMM EM, threshold scan.  Runs in this process,
+    chunks of cells on ``n_threads`` threads (numpy releases the GIL in the array work)."""
+    Xs_all = standardize_rows(np.asarray(norm_cols, dtype=F32).T)
+    n = Xs_all.shape[0]
+    out = np.empty(n, np.float64)
+
+    def run(lo, hi):
+        Xs = Xs_all[lo:hi]
+        lab = np.empty(Xs.shape, np.int8)
+        for j in range(hi - lo):
+            if labels is None or labels[lo + j][0] < 0:
+                lab[j] = exact_kmeans_labels(Xs[j])
+            else:
+                lab[j] = labels[lo + j]
+        dist = _distinct(Xs)
+        mu = exact_gmm_means(Xs, lab, distinct=dist)
+        for j in range(hi - lo):
+            out[lo + j] = exact_scan(Xs[j], mu[j, 0], mu[j, 1], distinct=(dist[0][j], dist[1][j]))
+
+    spans = [(i, min(n, i + chunk)) for i in range(0, n, chunk)]
+    if n_threads <= 1 or len(spans) == 1:
+        for lo, hi in spans:
+            run(lo, hi)
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=min(n_threads, len(spans)), thread_name_prefix="pert-tau") as ex:
+            for f in [ex.submit(run, lo, hi) for lo, hi in spans]:
+                f.result()
+    return out
+
+
+def default_threads() -> int:
+    """Threads of the exact host path: the affinity cores, at most 16."""
+    return max(1, min(16, len(os.sched_getaffinity(0))))
 
 
 def guess_times_batched(reads: np.ndarray, cn_states: np.ndarray, upsilon: float = 6, device=None,
-                        n_jobs: int = -1):
-    """pert_model.py:426-457: (t_init, t_alpha_prior, t_beta_prior), all cells at once; the
-    fragile cells (module doc) through the reference's per-cell path, on ``n_jobs``
-    processes (-1: the affinity cores, at most 16) when there are many."""
+                        n_threads: int = None):
+    """pert_model.py:426-457: (t_init, t_alpha_prior, t_beta_prior), all cells at once.
+    The batched fp64 pass (device) decides every cell whose result fp32 rounding cannot
+    change; the others take the exact host path (exact_fractions) -- with the batched
+    k-means labels where the partition is certain, else with sklearn's own k-means -- so
+    every cell's t_init is the reference's.  No worker processes."""
     dev = torch.device(device) if device is not None else torch.device("cpu")
-    x = torch.as_tensor(np.asarray(reads, np.float32), device=dev)
-    st = torch.as_tensor(np.asarray(cn_states, np.float32), device=dev)
-    norm = x / torch.where(st > 0.0, st, torch.full_like(st, 0.5))  # fp32, as the reference divides
-    frac, decisions, near = binarization_fraction(norm, return_fragile=True, return_minor=True)
+    x = torch.as_tensor(np.asarray(reads, np.float32))
+    st = torch.as_tensor(np.asarray(cn_states, np.float32))
+    # the reference's normalisation (:446-448), on the host in fp32 (these are the values
+    # the exact path standardises); the batched pass reads the same values on the device
+    norm = x / torch.where(st > 0.0, st, (torch.ones(x.shape) * 0.5).type(torch.float32))
+    frac, lab_unsure, near, lab = binarization_fraction(norm.to(dev), return_fragile=True, return_minor=True)
     t = frac.to(torch.float32).cpu().numpy()
-    L = norm.shape[0]
-    # Up to MINOR_EXACT_MAX_L bins every flagged cell goes through the reference's per-cell
-    # path (the result is the reference's).  Above, the finer near-ties are common (half the
-    # cells at 5,451 bins: the scan's minimum is flat against fp32 summation noise there, so
-    # the reference's own choice is not stable across BLAS builds either) and each per-cell
-    # fit takes about a second, so only the branch decisions are recomputed; the cells kept
-    # are counted in guess_times_batched.last_near_kept.
-    fragile = decisions | near if L <= MINOR_EXACT_MAX_L else decisions
-    guess_times_batched.last_near_kept = 0 if L <= MINOR_EXACT_MAX_L else int((near & ~decisions).sum())
-    redo = np.flatnonzero(fragile.cpu().numpy())
+    redo = np.flatnonzero((lab_unsure | near).cpu().numpy())
     if redo.size:
-        from .prep import manhattan_binarization
-        cols = norm[:, torch.as_tensor(redo, device=dev)].cpu().numpy()
-        jobs = [cols[:, j].reshape(-1, 1) for j in range(redo.size)]
-        # worker processes only where the per-cell fits outweigh their start-up: more than 64
-        # genome-scale cells' worth of bins, or a few cells once the pool is already warm
-        state = _pool_state(n_jobs)
-        big = redo.size * L > 64 * 5451
-        if n_jobs != 1 and redo.size > 4 and (big or state == "ready"):
-            if state == "warming":
-                _WARM[_pool_size(n_jobs)].join()    # never two executors being built at once
-            from joblib import Parallel, delayed
-            res = Parallel(n_jobs=_pool_size(n_jobs))(delayed(manhattan_binarization)(c) for c in jobs)
-        else:
-            res = [manhattan_binarization(c) for c in jobs]
-        for j, n in enumerate(redo):
-            t[n] = np.float32(res[j][1])
+        sel = torch.as_tensor(redo, device=lab.device)
+        labels = lab[:, sel].T.to(torch.int8).cpu().numpy()
+        labels[lab_unsure[sel].cpu().numpy()] = -1            # k-means recomputed on the host
+        nt = default_threads() if n_threads is None else int(n_threads)
+        fr = exact_fractions(norm[:, torch.as_tensor(redo)].numpy(), labels, n_threads=nt)
+        t[redo] = fr.astype(np.float32)
+        guess_times_batched.last_kmeans = int((labels[:, 0] < 0).sum())
+    else:
+        guess_times_batched.last_kmeans = 0
     guess_times_batched.last_fragile = redo
     alpha = (t * np.float32(upsilon)).astype(np.float32)
     return t, alpha, (np.float32(upsilon) - alpha).astype(np.float32)

@@ -34,7 +34,6 @@ def _fit(**extra):
     s, g = _tables()
     m = pert_infer_scRT(s, g, input_col='reads', clone_col='clone_id', cn_prior_method='g1_clones',
                         max_iter=120, min_iter=30, max_iter_step1=80, max_iter_step3=60, **extra)
-    m.tau_pool_jobs = 1                   # the ranks' per-cell tau path in-process (no worker pools)
     return m.run_pert_model()
 
 

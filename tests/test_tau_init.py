@@ -1,5 +1,12 @@
-"""Batched guess_times (tau_init.py) against the per-cell sklearn restatement of the
-reference's manhattan_binarization (prep.manhattan_binarization, pert_model.py:364-423)."""
+"""guess_times (tau_init.py) against the per-cell sklearn restatement of the reference's
+manhattan_binarization / guess_times (prep.manhattan_binarization, prep.guess_times:
+pert_model.py:364-457).
+
+Each stage of the exact host path is checked bit for bit against the sklearn call it
+restates (k-means labels, GMM means, standardisation), the exact path alone against the
+per-cell reference for every cell, and the product entry point (batched pass + exact path
+for the flagged cells) against the per-cell reference on >= 256 cells x 5,451 bins.
+"""
 import numpy as np
 import pytest
 import torch
@@ -15,6 +22,17 @@ def _profiles(n_s=60, n_g=30, L=500, seed=0):
     return reads, states
 
 
+def _norm(reads, states):
+    """The reference's CN normalisation (pert_model.py:446-448), fp32 torch on the host."""
+    x, st = torch.as_tensor(reads), torch.as_tensor(states)
+    return (x / torch.where(st > 0.0, st, (torch.ones(x.shape) * 0.5).type(torch.float32))).numpy()
+
+
+def _ref_standardized(col):
+    X = col.reshape(-1, 1)
+    return (X - np.mean(X)) / np.std(X)                      # pert_model.py:367
+
+
 def test_rng_draws_match_sklearn_kmeanspp():
     from sklearn.cluster import kmeans_plusplus
     rng = np.random.default_rng(3)
@@ -26,7 +44,6 @@ def test_rng_draws_match_sklearn_kmeanspp():
 
 
 def test_kmeanspp_matches_sklearn():
-    import torch
     from sklearn.cluster import kmeans_plusplus
     rng = np.random.default_rng(4)
     cols = [np.concatenate([rng.normal(0, 1, 150), rng.normal(3, 0.5, 90)]) for _ in range(20)]
@@ -39,40 +56,79 @@ def test_kmeanspp_matches_sklearn():
         np.testing.assert_allclose(c[:, n], cen[:, 0])
 
 
-@pytest.mark.parametrize("seed,L", [(0, 500), (6, 271), (8, 5451)])
-def test_batched_guess_times_matches_sklearn_per_cell(seed, L):
-    """Every cell's t_init equals the reference's per-cell sklearn result: the batched pass
-    decides the robust cells, the fragile ones (decisions within fp32 rounding of a tie)
-    go through the per-cell path.  (seed 8, 5,451 bins holds a cell whose scan optimum sits
-    on a data point, and k-means ties of identical read values occur in every set.)  Above
-    tau_init.MINOR_EXACT_MAX_L bins only branch decisions are recomputed and the finer
-    near-ties are kept (guess_times_batched.last_near_kept); on this set they still agree."""
-    reads, states = _profiles(n_s=60 if L < 5000 else 40, n_g=30 if L < 5000 else 20, L=L, seed=seed)
-    t_b, a_b, b_b = tau_init.guess_times_batched(reads, states, upsilon=6, n_jobs=1)
+@pytest.mark.parametrize("L,seed", [(271, 3), (5451, 21)])
+def test_exact_stages_match_sklearn_bit_for_bit(L, seed):
+    """standardize_rows == the per-cell standardisation; exact_kmeans_labels == KMeans
+    labels as GaussianMixture's initialisation runs it; exact_gmm_means ==
+    GaussianMixture(n_components=2, random_state=0).means_ (every bit)."""
+    from sklearn.cluster import KMeans
+    from sklearn.mixture import GaussianMixture
+    reads, states = _profiles(n_s=36 if L > 1000 else 60, n_g=12 if L > 1000 else 20, L=L, seed=seed)
+    norm = _norm(reads, states)
+    Xs = tau_init.standardize_rows(norm.T)
+    labs = np.empty(Xs.shape, np.int8)
+    ref_means = np.empty((Xs.shape[0], 2), np.float32)
+    for n in range(Xs.shape[0]):
+        X = _ref_standardized(norm[:, n])
+        np.testing.assert_array_equal(Xs[n], X[:, 0])
+        km = KMeans(n_clusters=2, n_init=1, random_state=np.random.RandomState(0)).fit(X).labels_
+        labs[n] = tau_init.exact_kmeans_labels(Xs[n])
+        np.testing.assert_array_equal(labs[n], km)
+        gm = GaussianMixture(n_components=2, random_state=0)
+        gm.fit_predict(X)
+        ref_means[n] = gm.means_[:, 0]
+    np.testing.assert_array_equal(tau_init.exact_gmm_means(Xs, labs), ref_means)
+
+
+@pytest.mark.parametrize("L,seed", [(271, 6), (5451, 9)])
+def test_exact_path_alone_matches_reference_every_cell(L, seed):
+    """Every cell through the exact host path (k-means on the host too), on 4 threads:
+    t_init equals the per-cell reference's for every cell."""
+    reads, states = _profiles(n_s=48 if L > 1000 else 80, n_g=16 if L > 1000 else 40, L=L, seed=seed)
+    fr = tau_init.exact_fractions(_norm(reads, states), None, n_threads=4, chunk=16).astype(np.float32)
+    t_r = prep.guess_times(reads, states, upsilon=6)[0]
+    np.testing.assert_array_equal(fr, t_r)
+
+
+@pytest.mark.parametrize("seed,L,n_s,n_g", [(0, 500, 60, 30), (6, 271, 60, 30), (11, 5451, 192, 64)])
+def test_batched_guess_times_matches_sklearn_per_cell(seed, L, n_s, n_g):
+    """The product entry point (batched pass, exact host path for the flagged cells) equals
+    the reference's per-cell result for every cell -- 256 cells x 5,451 bins included."""
+    reads, states = _profiles(n_s=n_s, n_g=n_g, L=L, seed=seed)
+    t_b, a_b, b_b = tau_init.guess_times_batched(reads, states, upsilon=6)
     t_r, a_r, b_r = prep.guess_times(reads, states, upsilon=6)
     np.testing.assert_array_equal(t_b, t_r)
     np.testing.assert_array_equal(a_b, a_r)
     np.testing.assert_allclose(a_b + b_b, 6.0, rtol=1e-6)
-    assert len(tau_init.guess_times_batched.last_fragile) < reads.shape[1]    # not all through sklearn
+    assert len(tau_init.guess_times_batched.last_fragile) < reads.shape[1]    # not all on the host path
 
 
-def test_fragile_cells_same_on_the_worker_pool_and_in_process(monkeypatch):
-    """The fragile cells' per-cell path gives the same t_init in-process and on a warm worker
-    pool (the paths guess_times_batched picks by problem size and pool state)."""
-    from scdna_replication_tools_amd import tau_init
+def test_exact_path_threads_and_forced_kmeans_agree(monkeypatch):
+    """Every cell flagged (k-means recomputed on the host): the same t_init on 1 and 3
+    threads, and equal to the per-cell reference."""
     from scdna_replication_tools_amd.simulator import simulate
-    sim = simulate(n_s=12, n_g=12, n_bins=300, num_reads=183 * 300, seed=2)
+    sim = simulate(n_s=40, n_g=12, n_bins=300, num_reads=183 * 300, seed=2)
     real = tau_init.binarization_fraction
 
-    def all_fragile(x, return_fragile=False, return_minor=False):
-        f, d, n = real(x, return_fragile=True, return_minor=True)
-        return f, torch.ones_like(d), torch.zeros_like(n)
+    def all_flagged(x, return_fragile=False, return_minor=False):
+        f, lab_unsure, near, lab = real(x, return_fragile=True, return_minor=True)
+        return f, torch.ones_like(lab_unsure), near, lab
 
-    monkeypatch.setattr(tau_init, "binarization_fraction", all_fragile)
-    t1 = tau_init.guess_times_batched(sim.reads_s, sim.cn_s, 6, device="cpu", n_jobs=1)[0]
-    assert len(tau_init.guess_times_batched.last_fragile) == 12
-    tau_init.prewarm_pool(2)
-    tau_init._WARM[2].join()
-    assert tau_init._pool_state(2) == "ready"
-    t2 = tau_init.guess_times_batched(sim.reads_s, sim.cn_s, 6, device="cpu", n_jobs=2)[0]
-    np.testing.assert_array_equal(t1, t2)
+    monkeypatch.setattr(tau_init, "binarization_fraction", all_flagged)
+    t1 = tau_init.guess_times_batched(sim.reads_s, sim.cn_s, 6, device="cpu", n_threads=1)[0]
+    assert len(tau_init.guess_times_batched.last_fragile) == 40
+    assert tau_init.guess_times_batched.last_kmeans == 40
+    t3 = tau_init.guess_times_batched(sim.reads_s, sim.cn_s, 6, device="cpu", n_threads=3)[0]
+    np.testing.assert_array_equal(t1, t3)
+    np.testing.assert_array_equal(t1, prep.guess_times(sim.reads_s, sim.cn_s, 6)[0])
+
+
+def test_no_worker_processes_in_the_product_path():
+    """The tau initialiser and the fit never start worker processes (joblib / loky /
+    multiprocessing) from the process that drives the GPU."""
+    import inspect
+    from scdna_replication_tools_amd import pert_model
+    for mod in (tau_init, pert_model, prep):
+        src = inspect.getsource(mod)
+        for word in ("joblib", "loky", "multiprocessing", "ProcessPool"):
+            assert word not in src, (mod.__name__, word)

@@ -75,6 +75,31 @@ def synth(n_total: int, subdivide: int, seed: int, device, num_reads: float = 1e
     return dict(gc=gc, reads=reads.float(), cn=cn.to(torch.int64), tau=tau.float(), clone_prof=prof, clone=clone)
 
 
+def composite_problem(n_total: int, seed: int = 0, n_g: int = 600, call_noise: float = 0.02):
+    """configs[3] with the reference's DEFAULT prior, g1_composite (pert_model.py:40, :299-361):
+    simulated S and G1/2 tables (numpy simulator, 3 clones, 1e6 reads per cell) whose G1/2
+    HMMcopy-style state calls disagree with the clone profile at ``call_noise`` of the bins
+    (+-1), through the product's own prep (pivots, consensus profiles, per-cell Pearson
+    matches to the clone's G1/2 cells, J = 5): eta is the product's composite code book --
+    many distinct rows, so the pass reads each row from the table in global memory.
+    Returns (reads (L, N) fp32, gc, eta, t_init, describe)."""
+    from scdna_replication_tools_amd import prep
+    from scdna_replication_tools_amd.pert_model import pert_infer_scRT
+    from scdna_replication_tools_amd.simulator import simulate, to_long_form
+    sim = simulate(n_s=n_total, n_g=n_g, n_clones=3, num_reads=1e6, seed=seed)
+    rng = np.random.default_rng(seed + 1)
+    flip = rng.random(sim.cn_g.shape) < call_noise
+    step = np.where(rng.random(sim.cn_g.shape) < 0.5, -1, 1)
+    sim.cn_g[:] = np.where(flip, np.clip(sim.cn_g + step, 0, P - 1), sim.cn_g)
+    df_s, df_g = to_long_form(sim, n_libs=1)
+    m = pert_infer_scRT(df_s, df_g, cn_prior_method="g1_composite", device="cpu", log_steps=False)
+    inp = m._prepare()
+    profiles = prep.consensus_clone_profiles(m.cn_g1, m.cn_state_col, keys=inp.keys_g)
+    eta = m._build_etas(inp, profiles)
+    t_init = np.full(inp.reads_s.shape[1], 0.5, np.float32)
+    return inp.reads_s.astype(np.float32), inp.gc, eta, t_init
+
+
 def cpu_share():
     """CPUs this process may use: its sched_getaffinity set, capped by a cgroup CPU quota
     (cpu.max) when one is set; plus the lscpu model name."""
@@ -256,6 +281,9 @@ def main():
     ap.add_argument("--cells", type=int, default=0, help="override the config's cell count (per job)")
     ap.add_argument("--subdivide", type=int, default=0, help="override the config's bin subdivision")
     ap.add_argument("--reads-per-cell", type=float, default=1e6, help="synthetic library size per cell")
+    ap.add_argument("--prior", default="g1_clones", choices=["g1_clones", "g1_composite"],
+                    help="CN prior of the step-2 fit: g1_clones (the tutorial's; one code per clone state) or "
+                         "g1_composite (the reference's default; the product's composite code book, many rows)")
     ap.add_argument("--cpu-cells", type=int, default=640)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -299,15 +327,28 @@ def main():
         n_cells = args.cells
         desc = "synthetic {} cells x {} bins (override of {})".format(n_cells, 5451 * subdiv, args.config)
     n_total = n_cells * (world if args.scaling == "weak" else 1)
-    data = synth(n_total, subdiv, seed=0, device=device, num_reads=args.reads_per_cell)
-    L = data["reads"].shape[0]
     n0, n1 = cell_bounds(n_total, world)[rank]
-    reads = data["reads"][:, n0:n1].cpu().numpy()
-    states = data["cn"][:, n0:n1].cpu().numpy()
-    eta = EtaCodebook.from_states(states, 1e6, P)                     # g1_clones prior (pert_model.py:285-296)
     bm = np.zeros((1, K + 1))
     bm[0, K - 1] = 0.5                                                # betas [0.5, 0] of the simulator
-    t_init = np.clip(data["tau"][n0:n1].cpu().numpy(), 0.05, 0.95)
+    if args.prior == "g1_composite":
+        if args.fit == "step1" or subdiv != 1:
+            raise SystemExit("--prior g1_composite: the step-2/3 fits at 500 kb")
+        reads_all, gc_all, eta_all, t_all = composite_problem(n_total)
+        L = reads_all.shape[0]
+        reads = np.ascontiguousarray(reads_all[:, n0:n1])
+        eta = EtaCodebook(np.ascontiguousarray(eta_all.codes[:, n0:n1]), eta_all.table)
+        t_init = t_all[n0:n1]
+        data = {"gc": gc_all}
+        states = None
+        prior_desc = "g1_composite (J=5, weight 1e5; {} distinct eta rows)".format(eta_all.table.shape[0])
+    else:
+        data = synth(n_total, subdiv, seed=0, device=device, num_reads=args.reads_per_cell)
+        L = data["reads"].shape[0]
+        reads = data["reads"][:, n0:n1].cpu().numpy()
+        states = data["cn"][:, n0:n1].cpu().numpy()
+        eta = EtaCodebook.from_states(states, 1e6, P)                 # g1_clones prior (pert_model.py:285-296)
+        t_init = np.clip(data["tau"][n0:n1].cpu().numpy(), 0.05, 0.95)
+        prior_desc = "g1_clones (weight 1e6)"
     ploidy = eta.argmax_states().mean(0)
     allreduce = make_allreduce()
     libs = np.zeros(n1 - n0, int)
@@ -389,7 +430,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
             "scaling": args.scaling, "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": desc, "config": args.config, "cells": n_total, "bins": L, "P": P,
-                       "K": K, "cn_prior": "g1_clones (weight 1e6)", "parallelism": "cell-sharded x{}".format(world),
+                       "K": K, "cn_prior": prior_desc, "parallelism": "cell-sharded x{}".format(world),
                        "bins_per_tile": shard.bins_per_tile, "fit": args.fit},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
@@ -427,7 +468,7 @@ def main():
                 p = pn["pmc"]
                 if p.get("SQ_ACTIVE_INST_ANY"):
                     rec["roofline"]["wait_inst_frac"] = p.get("SQ_WAIT_INST_ANY", 0.0) / p["SQ_ACTIVE_INST_ANY"]
-        if world == 1 and not args.no_cpu_baseline and args.fit == "step2":
+        if world == 1 and not args.no_cpu_baseline and args.fit == "step2" and args.prior == "g1_clones":
             data = synth(max(args.cpu_cells, 3), subdiv, seed=0, device=device)
             rec["cpu_baseline"] = cpu_baseline(data, args.cpu_cells, args.cpu_steps)
         else:

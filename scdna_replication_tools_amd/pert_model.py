@@ -467,6 +467,7 @@ class pert_infer_scRT():
             # ---- step 2: S cells, enumerated (:776-830)
             tic = time.perf_counter()
             profiles, etas, t_init, (t_priors, t_guess) = fut_priors.result()
+            self.t_init_s = t_init                 # step 2's tau initialisation (:790), for inspection
             # wall time step 1 did not hide (the helper's own durations: timings["helper_*"])
             self.timings["guess_times_s"] = time.perf_counter() - tic
             self.timings["helper_priors"], self.timings["helper_guess_times_s"] = t_priors, t_guess
@@ -495,6 +496,7 @@ class pert_infer_scRT():
                 # ---- step 3: G1 cells with rho, a frozen (:834-896)
                 tic = time.perf_counter()
                 etas2, t_init2 = fut_prep3.result()
+                self.t_init_g = t_init2
                 ploidy2 = etas2.argmax_states().astype(np.float32).mean(0)
                 self.timings["prep_step3"] = time.perf_counter() - tic      # the part step 2 did not hide
                 init3 = init_params(KIND_STEP3, inp.reads_g, inp.libs_g, n_libs, P, K, ploidy=ploidy2,

@@ -179,8 +179,19 @@ def check(name: str, g_dev, g64, floor) -> float:
     return worst
 
 
-def check_all(prob: po.OracleProblem, z: dict, g_dev: dict, g64: dict, skip=()) -> dict:
-    """``check`` for every site of g64; returns {site: worst ratio}."""
+def floor_stats(g64, floor) -> dict:
+    """How loose the floor is: floor / |g64| over the elements (median, p99, max) and the
+    fraction of elements where the floor, not RTOL |g64|, sets the bound."""
+    g = np.abs(np.asarray(g64, np.float64)).reshape(-1)
+    f = np.broadcast_to(np.asarray(floor, np.float64), np.shape(g64)).reshape(-1)
+    r = f / np.maximum(g, 1e-300)
+    return {"floor_over_g64_median": float(np.median(r)), "floor_over_g64_p99": float(np.percentile(r, 99)),
+            "floor_over_g64_max": float(r.max()), "floor_dominant_frac": float((f > RTOL * g).mean())}
+
+
+def check_all(prob: po.OracleProblem, z: dict, g_dev: dict, g64: dict, skip=(), report: dict = None) -> dict:
+    """``check`` for every site of g64; returns {site: worst ratio}.  With ``report``, also
+    records per site the worst ratio, the tensor rel-L2 error and the floor statistics."""
     A = contribution_scale(prob, z)
     S = score_sensitivity(prob, z) if prob.kind != "step1" else {}
     out = {}
@@ -191,5 +202,36 @@ def check_all(prob: po.OracleProblem, z: dict, g_dev: dict, g64: dict, skip=()) 
         floor = pi_floor(prob, z) if name == "expose_pi" else FLOOR_C * A[name].reshape(ref.shape)
         if name in S:
             floor = floor + S[name].reshape(ref.shape)
+        if report is not None:
+            gd = np.asarray(g_dev[name], np.float64).reshape(ref.shape)
+            report[name] = dict(rel_l2=rel_l2(gd, ref), **floor_stats(ref, floor))
         out[name] = check(name, g_dev[name], ref, floor)
+        if report is not None:
+            report[name]["worst_delta_over_bound"] = out[name]
     return out
+
+
+def rel_l2(a, b) -> float:
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def write_report(case: str, entry: dict, path: str = None):
+    """Merge ``entry`` under ``case`` into the JSON parity report (default
+    gpurun_out/parity_report.json, or $PERT_PARITY_REPORT)."""
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = path or os.environ.get("PERT_PARITY_REPORT", os.path.join(root, "gpurun_out", "parity_report.json"))
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    data = {}
+    if os.path.exists(path):
+        try:
+            with open(path) as fh:
+                data = json.load(fh)
+        except ValueError:
+            data = {}
+    data[case] = entry
+    with open(path, "w") as fh:
+        json.dump(data, fh, indent=1, sort_keys=True)

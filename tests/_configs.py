@@ -42,3 +42,27 @@ def input_digest(*frames) -> str:
             h.update(c.encode())
             h.update(np.ascontiguousarray(f[c].astype(str).to_numpy().astype("U")).tobytes())
     return h.hexdigest()[:16]
+
+
+GENOME_KW = dict(input_col='reads', clone_col='clone_id', assign_col='copy', rt_prior_col=None, cn_state_col='state',
+                 gc_col='gc', cn_prior_method='g1_clones')
+
+
+def genome_tables(seed: int = 7, n_s: int = 64, n_g: int = 64):
+    """configs[2]-style genome-length sample (test_gpu_chain's genome fixture): the full
+    5,451-bin 500 kb grid, 3 clones, 1e6 reads per cell, two libraries; (cn_s, cn_g1, truth_s)."""
+    from scdna_replication_tools_amd.simulator import simulate, to_long_form
+    sim = simulate(n_s=n_s, n_g=n_g, n_clones=3, num_reads=1e6, seed=seed)
+    df_s, df_g = to_long_form(sim, n_libs=2)
+    truth = df_s[['cell_id', 'chr', 'start', 'true_somatic_cn', 'true_rep']].copy()
+    keep_s = ['cell_id', 'chr', 'start', 'end', 'gc', 'state', 'copy', 'reads', 'library_id', 'clone_id']
+    keep_s = [c for c in keep_s if c in df_s.columns]
+    keep_g = [c for c in keep_s if c in df_g.columns]
+    return df_s[keep_s].copy(), df_g[keep_g].copy(), truth
+
+
+def genome_scrt(cn_s, cn_g1, **extra):
+    """The reference's entry point with its defaults (max_iter 2000, min_iter 100, rel_tol
+    1e-6, steps 1 / 3 at half) on the genome-length sample, g1_clones prior."""
+    from scdna_replication_tools.infer_scRT import scRT
+    return scRT(cn_s, cn_g1, **GENOME_KW, **extra)

@@ -109,3 +109,34 @@ def test_tutorial_cell9_verbatim_matches_chained_oracle_fixture():
     # and the fit finds the simulated states
     m = cn_s_with_scrt.merge(truth, on=['cell_id', 'chr', 'start'])
     assert (m['model_cn_state'] == m['true_somatic_cn']).mean() > 0.99
+
+
+GENOME = os.path.join(os.path.dirname(__file__), "golden", "genome_chain_oracle.npz")
+
+
+def test_genome_length_chain_matches_oracle_fixture():
+    """configs[2]-style genome-length sample (64 S + 64 G1/2 cells x 5,451 bins, 3 clones,
+    two libraries) through the reference's entry point with its defaults
+    (``scRT(...).infer(level='pyro')``: max_iter 2000 / min_iter 100 / rel_tol 1e-6, steps
+    1 and 3 at half) against the committed fp32 oracle chain
+    (tests/golden/make_genome_chain_golden.py): the same t_init for every cell (the exact
+    tau initialiser), the same stopping iteration of every fit, loss traces within 1e-4,
+    decodes >= 99.9 %, final sites close."""
+    from tests._configs import genome_scrt, genome_tables, input_digest
+    if not os.path.exists(GENOME):
+        pytest.skip("tests/golden/genome_chain_oracle.npz not generated (tests/golden/make_genome_chain_golden.py)")
+    fx = dict(np.load(GENOME))
+    s, g, truth = genome_tables()
+    assert input_digest(s, g) == str(fx["input_digest"]), "genome inputs changed"
+    scrt = genome_scrt(s, g)
+    out = scrt.infer(level='pyro')
+    inp = scrt.model._prepare()
+    assert list(inp.cells_s) == list(fx["cells_s"]) and list(inp.cells_g) == list(fx["cells_g"])
+    np.testing.assert_array_equal(scrt.model.t_init_s, fx["t_init_s"])
+    np.testing.assert_array_equal(scrt.model.t_init_g, fx["t_init_g"])
+    prod = product_arrays(scrt.model, *out)
+    rep = _compare(prod, fx)
+    from tests import _bounds
+    _bounds.write_report("genome_chain_64x64x5451", {k: (list(v) if isinstance(v, tuple) else v) for k, v in rep.items()})
+    m = out[0].merge(truth, on=['cell_id', 'chr', 'start'])
+    assert (m['model_cn_state'] == m['true_somatic_cn']).mean() > 0.99

@@ -1,5 +1,8 @@
-"""Summarise a tools/profile.sh run: per-kernel average duration (kernel trace) and
-per-dispatch averages of every PMC counter, plus HBM traffic per launch.
+"""Summarise a tools/profile.sh run: per-kernel average duration (kernel-trace stats), the
+median and warm-up-excluded mean duration over the trace's dispatches (the first
+``WARMUP_FRAC`` of each kernel's dispatches dropped: cold first launches would otherwise
+lift the average above the bench's own step time), per-dispatch averages of every PMC
+counter, plus HBM traffic per launch.
 
 HBM bytes per launch (MI355X_MICROARCH.md, HBM section): read bytes from the L2
 memory-side request counters by request size (TCC_EA0_RDREQ_{32B,64B,128B}); FETCH_SIZE
@@ -22,8 +25,30 @@ def short(name):
     return None
 
 
+WARMUP_FRAC = 0.2
+
+
+def trace_durations(d):
+    """{kernel: [durations in ns, in dispatch order]} from the kernel trace."""
+    dur = defaultdict(list)
+    for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_trace.csv"), recursive=True):
+        rows = list(csv.DictReader(open(f)))
+        rows.sort(key=lambda r: int(r.get("Dispatch_Id", 0) or 0))
+        for row in rows:
+            k = short(row.get("Kernel_Name", ""))
+            if k:
+                dur[k].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    return dur
+
+
 def main(d):
     out = {"kernels": {}}
+    for k, ds in trace_durations(d).items():
+        warm = ds[int(len(ds) * WARMUP_FRAC):] or ds
+        ent = out["kernels"].setdefault(k, {})
+        ent["median_ns"] = float(sorted(ds)[len(ds) // 2])
+        ent["warm_mean_ns"] = float(sum(warm) / len(warm))
+        ent["dispatches"] = len(ds)
     stats = glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True)
     for f in stats:
         for row in csv.DictReader(open(f)):

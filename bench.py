@@ -355,13 +355,13 @@ def main():
     common = dict(device=device, is_root=(rank == 0), allreduce=allreduce, bins_per_tile=args.bins_per_tile,
                   variant=args.variant, fused=args.fused and not args.no_fused)
     if args.fit == "step1":
-        # step 1 (pert_model.py:718-774): the same cells as G1/2 cells, doubled with rep 0 / 1
-        st2 = np.concatenate([states, states], 1)
-        rd2 = np.concatenate([reads, reads], 1)
-        rep2 = np.concatenate([np.zeros_like(states), np.ones_like(states)], 1)
-        init = init_params(1, rd2, np.zeros(2 * (n1 - n0), int), 1, P, K, seed=0)
-        shard = PertShard(1, rd2, data["gc"], np.zeros(2 * (n1 - n0), int), 1, P, K, init, cn_obs=st2,
-                          rep_obs=rep2, n_cells_total=2 * n_total, **common)
+        # step 1 (pert_model.py:718-774): the same cells as G1/2 cells, doubled with rep 0 / 1 --
+        # as the product runs it, in pair mode (the columns stored once, both copies per lane)
+        mr = reads.astype(np.float64).mean(0)
+        init = init_params(1, None, np.zeros(2 * (n1 - n0), int), 1, P, K, seed=0,
+                           mean_reads=np.concatenate([mr, mr]), n_bins=L)
+        shard = PertShard(1, reads, data["gc"], np.zeros(2 * (n1 - n0), int), 1, P, K, init, cn_obs=states,
+                          paired=True, n_cells_total=2 * n_total, **common)
     else:
         kind = 2 if args.fit == "step2" else 3
         init = init_params(kind, reads, libs, 1, P, K, ploidy=ploidy, t_init=t_init, beta_means=bm, seed=0)
@@ -407,7 +407,9 @@ def main():
         cellbins_total = L * n_total * (2 if args.fit == "step1" else 1)
         value = cellbins_total * args.steps / dt
         step1 = args.fit == "step1"
-        bpc = 4 + 1 + 1 if step1 else bytes_per_cellbin(P)      # step 1: reads + observed cn, rep (u8)
+        # step 1, pair mode: reads fp32 + observed cn u8 per G1/2 cell and bin, shared by its two
+        # copies (2.5 B per fitted cell and bin)
+        bpc = 2.5 if step1 else bytes_per_cellbin(P)
         local_cb = L * (n1 - n0) * (2 if step1 else 1)
         achieved = bpc * local_cb / (kern_ms * 1e-3) / 1e9
         kname = ("obs_kernel" if step1 else

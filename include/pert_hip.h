@@ -30,6 +30,12 @@
  *                                   contiguous run over its bins)
  *   cn_obs/rep_obs, cn_out/rep_out uint8 [L][ldn]
  *   packed params (unconstrained, see pert_layout below), float
+ *
+ * Step 1 pair mode (rep_obs == NULL): the training set of pert_model.py:228-251 -- every
+ * G1/2 cell twice, rep 0 then rep 1, same reads and CN -- stored once: N is even, cells
+ * [0, N/2) are the rep-0 copies and [N/2, N) the rep-1 copies of the N/2 columns that reads
+ * and cn_obs hold, whose row stride ldn (>= N/2, multiple of 256) is that of the stored
+ * arrays.  Parameters, libs, mean_reads, ploidy and the workspace stay per cell (N).
  */
 #ifndef PERT_HIP_H
 #define PERT_HIP_H
@@ -187,7 +193,9 @@ int pert_enum_step(const pert_problem* prob, pert_state* st, const pert_adam_hpa
 int pert_adam_shared(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
                      hipStream_t stream);
 
-/* Observed (step 1) pass: JitTrace_ELBO forward + backward of pert_model.py:743. */
+/* Observed (step 1) pass: JitTrace_ELBO forward + backward of pert_model.py:743.  In pair
+ * mode (rep_obs == NULL, see the layouts above) one lane evaluates both copies of a G1/2 cell
+ * from one load of its reads and CN (bins_per_tile up to 128). */
 int pert_obs_pass(const pert_problem* prob, pert_state* st, hipStream_t stream);
 
 /* Reductions of the pass partials + priors of the non-enumerated sites (pert_model.py:553-603)

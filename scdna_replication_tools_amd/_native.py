@@ -113,7 +113,11 @@ def load(path: str):
             "{} not found: the PERT HIP extension is not built (run "
             "`python -m scdna_replication_tools_amd.build`). There is no CPU fallback.".format(path))
     try:
-        handle = ctypes.CDLL(path)
+        # PyDLL: the calls keep the GIL.  Every entry point returns in microseconds (launches,
+        # no synchronisation), and a thread that drops the GIL around each launch waits for it
+        # again behind whatever Python work another thread of the fit is doing (up to the
+        # interpreter's switch interval per call), which starves the device of queued steps.
+        handle = ctypes.PyDLL(path)
     except OSError as e:  # pragma: no cover
         raise NativeLibraryError("failed to load {}: {}".format(path, e))
     missing = [s for s in EXPORTED_SYMBOLS if not hasattr(handle, s)]

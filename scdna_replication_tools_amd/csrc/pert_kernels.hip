@@ -950,6 +950,159 @@ __global__ void __launch_bounds__(kBlock) obs_kernel(pert_problem pr, pert_state
 }
 
 // ------------------------------------------------------------------------------------------
+// Observed pass over PAIRS (step 1's training set, pert_model.py:228-251: every G1/2 cell twice,
+// rep 0 then rep 1, with the same reads and CN).  Pair mode (include/pert_hip.h): rep_obs is
+// NULL, cells [0, N/2) are the rep-0 copies and [N/2, N) the rep-1 copies, reads / cn_obs hold
+// the N/2 columns once.  One lane = one pair: the two copies' NB chains share the loads (5 B
+// per pair and bin instead of 12) and are independent, so each lane carries two dependency
+// chains -- the single-cell pass (obs_kernel) is latency-bound at ~0.3 VALU issue with its
+// waves waiting on their own chain 63 % of the time (profiles/r03b_s1).  One wave per
+// workgroup, no barrier in the bin loop; per-bin rho sums by a wave reduction, staged in LDS
+// and stored once per tile.
+constexpr int kMaxLTObs = 128;
+
+template <int K1T>
+__global__ void __launch_bounds__(64) obs_pair_kernel(pert_problem pr, pert_state st) {
+  if (loop_stopped(st)) return;
+  const int lane = threadIdx.x;
+  const int N = pr.N, NG = pr.N >> 1;
+  const int K1 = (K1T == PERT_MAX_K1) ? pr.K1 : K1T;
+  const int g = blockIdx.x * 64 + lane;
+  const bool valid = g < NG;
+  const int LT = st.bins_per_tile;
+  const int l0 = blockIdx.y * LT;
+  const int l1 = min(pr.L, l0 + LT);
+  const pert_layout lay = st.lay;
+
+  __shared__ float s_bc[kMaxLTObs * (K1T + 1)];
+  __shared__ float s_bin[kMaxLTObs];
+  // per-bin constants of the tile (constrained rho, GC features), requested first
+  for (int i = lane; i < (l1 - l0) * (K1 + 1); i += 64) {
+    const int lb = i / (K1 + 1), j = i - lb * (K1 + 1);
+    float dm;
+    s_bc[lb * (K1T + 1) + j] =
+        j == 0 ? clipped_sigmoid(st.params[lay.off_rho + l0 + lb], &dm) : pr.gcf[(l0 + lb) * K1 + j - 1];
+  }
+  const float a_val = fexp(st.params[lay.off_a]);
+  float dml;
+  const float lam = 0.001f + 0.998f * clipped_sigmoid(st.params[lay.off_lam], &dml);
+  const float c0 = (1.0f - lam) / lam;
+  const float log1m_lam = logf(1.0f - lam);
+
+  float ucc[2], tau[2], beta[2][K1T];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    ucc[r] = 0.0f;
+    tau[r] = 0.5f;
+#pragma unroll
+    for (int k = 0; k < K1T; ++k) beta[r][k] = 0.0f;
+    if (valid) {
+      const int n = g + r * NG;
+      ucc[r] = st.params[lay.off_u + n] * c0;
+#pragma unroll
+      for (int k = 0; k < K1T; ++k)
+        if (k < K1) beta[r][k] = st.params[lay.off_beta + k * N + n];
+      float dm;
+      tau[r] = clipped_sigmoid(st.params[lay.off_tau + n], &dm);
+    }
+  }
+  float acc[2][K1T], accT[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    accT[r] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < K1T; ++k) acc[r][k] = 0.0f;
+  }
+  float loss = 0.0f, ga = 0.0f, dsum = 0.0f, gdd = 0.0f;
+  __syncthreads();                                   // s_bc written by the wave's lanes
+
+  // register software pipeline: the reads and CN of the next kObsU bins are in flight while
+  // the current ones compute (rows padded to ldn: every lane may load)
+  constexpr int kObsU = 4;
+  const float* __restrict__ reads = pr.reads;
+  const uint8_t* __restrict__ cno = pr.cn_obs;
+  const size_t col = (size_t)(valid ? g : 0);
+  float xq[kObsU];
+  uint32_t cq[kObsU];
+  auto load_group = [&](int lg) {
+#pragma unroll
+    for (int u = 0; u < kObsU; ++u) {
+      const size_t ln = (size_t)min(lg + u, l1 - 1) * pr.ldn + col;
+      xq[u] = reads[ln];
+      cq[u] = cno[ln];
+    }
+  };
+  if (l0 < l1) load_group(l0);
+  for (int lg = l0; lg < l1; lg += kObsU) {
+    float xg[kObsU], cg[kObsU];
+#pragma unroll
+    for (int u = 0; u < kObsU; ++u) { xg[u] = xq[u]; cg[u] = (float)cq[u]; }
+    if (lg + kObsU < l1) load_group(lg + kObsU);
+#pragma unroll
+    for (int u = 0; u < kObsU; ++u) {
+      const int l = lg + u;
+      if (l >= l1) break;
+      const float x = xg[u], cnf = cg[u];
+      const float* bcl = s_bc + (l - l0) * (K1T + 1);
+      const float rho = bcl[0];
+      float gf[K1T];
+#pragma unroll
+      for (int k = 0; k < K1T; ++k) gf[k] = (k < K1) ? bcl[1 + k] : 0.0f;
+      const float invx = x > 0.0f ? frcp(x) : 0.0f;
+      float gt_sum = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        float dot = 0.0f;
+#pragma unroll
+        for (int k = 0; k < K1T; ++k) dot += beta[r][k] * gf[k];
+        const float omega = fexp(dot);
+        const float t = tau[r] - rho;
+        const float phi = 1.0f / (1.0f + fexp(-a_val * t));
+        ObsOut o;
+        obs_cellbin(x, invx, cnf, (float)r, log1m_lam, ucc[r] * omega, phi, o);
+        if (valid) {
+          loss += o.ll;
+          gt_sum += o.gt;
+          accT[r] += a_val * o.gt;
+          ga += t * o.gt;
+          dsum += o.dsum;
+          gdd += o.gdd;
+          const float ge = o.gD * omega;
+#pragma unroll
+          for (int k = 0; k < K1T; ++k) acc[r][k] += ge * gf[k];
+        }
+      }
+      const float ws = wave_sum(gt_sum);
+      if (lane == 0) s_bin[l - l0] = ws;
+    }
+  }
+  __syncthreads();
+  for (int i = lane; i < l1 - l0; i += 64) st.bin_part[(size_t)blockIdx.x * pr.L + l0 + i] = s_bin[i];
+  if (valid) {
+    float* cp = st.cell_part + (size_t)blockIdx.y * (K1 + 1) * N;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int n = g + r * NG;
+#pragma unroll
+      for (int k = 0; k < K1T; ++k)
+        if (k < K1) cp[(size_t)k * N + n] = acc[r][k];
+      cp[(size_t)K1 * N + n] = accT[r];
+    }
+  }
+  const double bl = wave_sum_d((double)loss);
+  const double bga = wave_sum_d((double)ga);
+  const double bds = wave_sum_d((double)dsum);
+  const double bgd = wave_sum_d((double)gdd);
+  if (lane == 0) {
+    double* bp = st.blk_part + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlkSlots;
+    bp[0] = bl;
+    bp[1] = bga;
+    bp[2] = bds;
+    bp[3] = bgd;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Per-cell and per-bin reductions + priors of the non-enumerated sites + the global sums,
 // one launch.  1024-thread workgroups = 64 items (lanes) x 16 groups (waves).  Blocks
 // [0, n_cblk) take 64 cells each: group g sums the per-cell partials [n_bt][CS][N] of bin
@@ -1816,8 +1969,23 @@ int tile_bins(const pert_state* st) {
   return lt > kMaxLT ? kMaxLT : lt;
 }
 
+// step 1 in pair mode (include/pert_hip.h): rep_obs NULL, the N/2 stored columns read twice
+bool pair_mode(const pert_problem* p) { return p->kind == PERT_KIND_STEP1 && p->rep_obs == nullptr; }
+
+// cell tiles of the observed pass: 256-cell workgroups, or 64-pair waves in pair mode
+int obs_cell_tiles(const pert_problem* pr) { return pair_mode(pr) ? (pr->N / 2 + 63) / 64 : pr->ldn / kBlock; }
+
+
+// the tile length a launch of this problem uses (the pair pass allows longer tiles)
+int tile_bins(const pert_problem* p, const pert_state* st) {
+  if (!pair_mode(p)) return tile_bins(st);
+  const int lt = st->bins_per_tile > 0 ? st->bins_per_tile : kDefaultLT;
+  return lt > kMaxLTObs ? kMaxLTObs : lt;
+}
+
 bool problem_ok(const pert_problem* p) {
-  return p && p->L > 0 && p->N > 0 && p->ldn >= p->N && p->ldn % PERT_BLOCK == 0 &&
+  return p && p->L > 0 && p->N > 0 && p->ldn % PERT_BLOCK == 0 &&
+         (pair_mode(p) ? (p->N % 2 == 0 && p->ldn >= p->N / 2) : p->ldn >= p->N) &&
          p->K1 >= 1 && p->K1 <= PERT_MAX_K1 && p->n_libs >= 1 &&
          p->P >= PERT_MIN_P && p->P <= PERT_MAX_P && p->reads && p->gcf && p->libs && p->mean_reads &&
          p->ploidy;
@@ -1966,11 +2134,34 @@ int pert_auto_bins_per_tile(const pert_problem* prob, int32_t variant, int32_t* 
     return PERT_E_ARG;
   if (!variant_ok(variant)) return PERT_E_ARG;
   *out = kDefaultLT;
-  if (prob->kind == PERT_KIND_STEP1) return PERT_OK;
+  if (prob->kind == PERT_KIND_STEP1 && !pair_mode(prob)) return PERT_OK;
   int dev = 0, ncu = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return hip_status(e);
+  if (prob->kind == PERT_KIND_STEP1) {
+    // pair pass: one-wave tiles of 64 pairs x lt bins.  Each tile also writes (and finalize
+    // reads) 2 (K1 + 1) partial floats per pair, against 5 B per pair and bin of input, so
+    // longer tiles cut traffic; but the launch takes ceil(tiles / slots) rounds and a last
+    // round that fills few slots idles most of the chip.  Least (rounds + 1/8) x (lt + 8),
+    // the 8 being the partials' cost in bins, over lt in [32, kMaxLTObs].
+    int nb = 0;
+    if (prob->K1 == 5)
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, obs_pair_kernel<5>, 64, 0);
+    else
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, obs_pair_kernel<PERT_MAX_K1>, 64, 0);
+    if (e != hipSuccess) return hip_status(e);
+    const long slots = (long)ncu * (nb > 0 ? nb : 16);
+    const long n_ct = obs_cell_tiles(prob);
+    long best = -1;
+    for (int lt = kMaxLTObs; lt >= 32; --lt) {
+      const long tiles = n_ct * ((prob->L + lt - 1) / lt);
+      const long rounds = (tiles + slots - 1) / slots;
+      const long cost = (8 * rounds + 1) * (lt + 8);
+      if (best < 0 || cost < best) { best = cost; *out = lt; }
+    }
+    return PERT_OK;
+  }
   // Each resident wave runs one tile (a prologue of about kTilePrologue bins plus lt bins);
   // the pass takes ceil(tiles / slots) such rounds, and the last round ends with a tail in
   // which the slowest waves finish their tiles: wave exits spread over about 1/8 of a tile
@@ -2066,20 +2257,25 @@ int pert_adam_shared(const pert_problem* prob, pert_state* st, const pert_adam_h
 
 int pert_obs_pass(const pert_problem* prob, pert_state* st, hipStream_t stream) {
   if (!problem_ok(prob) || !st || prob->kind != PERT_KIND_STEP1) return PERT_E_ARG;
-  if (!prob->cn_obs || !prob->rep_obs || !st->cell_part || !st->bin_part || !st->blk_part) return PERT_E_ARG;
+  if (!prob->cn_obs || !st->cell_part || !st->bin_part || !st->blk_part) return PERT_E_ARG;
   pert_state s2 = *st;
-  s2.bins_per_tile = tile_bins(st);
-  const dim3 grid((prob->N + kBlock - 1) / kBlock, (prob->L + s2.bins_per_tile - 1) / s2.bins_per_tile);
-  hipLaunchKernelGGL(obs_kernel, grid, dim3(kBlock), 0, stream, *prob, s2);
+  s2.bins_per_tile = tile_bins(prob, st);
+  const dim3 grid(obs_cell_tiles(prob), (prob->L + s2.bins_per_tile - 1) / s2.bins_per_tile);
+  if (!pair_mode(prob))
+    hipLaunchKernelGGL(obs_kernel, grid, dim3(kBlock), 0, stream, *prob, s2);
+  else if (prob->K1 == 5)
+    hipLaunchKernelGGL(obs_pair_kernel<5>, grid, dim3(64), 0, stream, *prob, s2);
+  else
+    hipLaunchKernelGGL(obs_pair_kernel<PERT_MAX_K1>, grid, dim3(64), 0, stream, *prob, s2);
   return hip_status(hipGetLastError());
 }
 
 int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream) {
   if (!problem_ok(prob) || !st || !st->grad_shared || !st->grad_cell || !st->cellblk_part) return PERT_E_ARG;
   pert_state s2 = *st;
-  s2.bins_per_tile = tile_bins(st);
+  s2.bins_per_tile = tile_bins(prob, st);
   const int lt = s2.bins_per_tile;
-  const int n_ct = prob->kind == PERT_KIND_STEP1 ? prob->ldn / kBlock : enum_cell_tiles(prob, st);
+  const int n_ct = prob->kind == PERT_KIND_STEP1 ? obs_cell_tiles(prob) : enum_cell_tiles(prob, st);
   const int n_bt = (prob->L + lt - 1) / lt;
   const int n_lblk = (prob->L + 63) / 64;
   const int n_cblk = (prob->N + 63) / 64;

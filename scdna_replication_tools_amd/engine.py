@@ -228,7 +228,7 @@ class PertShard:
                  is_root: bool = True, n_cells_total: Optional[int] = None,
                  allreduce: Optional[Callable[[torch.Tensor], None]] = None,
                  dirichlet_mode: str = "torch32", bins_per_tile: int = 0, variant: int = 3, fused: bool = False,
-                 lib=None):
+                 paired: bool = False, lib=None):
         self.lib = nat.lib() if lib is None else lib        # another build of the ABI (A/B tools)
         self.kind = int(kind)
         self.variant = int(variant)
@@ -240,7 +240,14 @@ class PertShard:
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         reads = np.asarray(reads)
-        L, N = reads.shape
+        # step 1 pair mode (include/pert_hip.h): ``reads`` / ``cn_obs`` hold the G1/2 cells once;
+        # the fit's cells are their rep-0 copies then their rep-1 copies (pert_model.py:228-251),
+        # so ``libs`` and the per-cell entries of ``init`` are per copy (twice the columns)
+        self.paired = bool(paired)
+        if self.paired and (self.kind != nat.KIND_STEP1 or rep_obs is not None):
+            raise ValueError("pair mode is step 1's doubled training set: kind 1, no rep_obs")
+        L, NS = reads.shape
+        N = 2 * NS if self.paired else NS
         self.L, self.N, self.P, self.K, self.K1, self.n_libs = L, N, int(P), int(K), int(K) + 1, int(n_libs)
         if not (nat.MIN_P <= self.P <= nat.MAX_P):
             raise ValueError("P={} unsupported (2..16)".format(P))
@@ -252,7 +259,7 @@ class PertShard:
         self.t = 0
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
-        self.ldn = ldn = -(-N // nat.BLOCK) * nat.BLOCK       # row stride: N rounded up to 256
+        self.ldn = ldn = -(-NS // nat.BLOCK) * nat.BLOCK      # row stride: stored columns rounded up to 256
 
         # ---- inputs (pert_model.py:133-191 layouts)
         self.reads = self._pad_rows(torch.as_tensor(reads.astype(F32)), dev)
@@ -260,6 +267,8 @@ class PertShard:
         self.libs = torch.as_tensor(np.asarray(libs).astype(np.int32), device=dev)
         x64 = reads.astype(np.float64)
         mean_reads = torch.mean(torch.as_tensor(reads, dtype=torch.float32), dim=0)
+        if self.paired:
+            mean_reads = torch.cat([mean_reads, mean_reads])
         self.mean_reads = mean_reads.to(dev)
         if self.kind == nat.KIND_STEP1:
             ploidy = np.full(N, 2.0, dtype=F32)                                       # :595
@@ -281,7 +290,8 @@ class PertShard:
             if cn.min() < 0 or cn.max() >= self.P:
                 raise ValueError("observed CN states must lie in [0, P)")
             self.cn_obs = self._pad_rows(torch.as_tensor(cn.astype(np.uint8)), dev)
-            self.rep_obs = self._pad_rows(torch.as_tensor(np.asarray(rep_obs).astype(np.uint8)), dev)
+            if not self.paired:
+                self.rep_obs = self._pad_rows(torch.as_tensor(np.asarray(rep_obs).astype(np.uint8)), dev)
         else:
             self.eta_code = self._pad_rows(
                 torch.as_tensor(np.ascontiguousarray(eta.codes, dtype=np.uint16).view(np.int16)), dev)
@@ -324,8 +334,9 @@ class PertShard:
 
         # ---- constants of the loss (added on the host, summed over ranks once)
         if self.kind == nat.KIND_STEP1:
-            const = kappa_sum(x64, None) + L * N * math.lgamma(self.P)   # Dirichlet(ones) normaliser
-            self.sum_reads = float(x64.sum())
+            copies = 2 if self.paired else 1
+            const = copies * kappa_sum(x64, None) + L * N * math.lgamma(self.P)   # Dirichlet(ones) normaliser
+            self.sum_reads = copies * float(x64.sum())
             self.pi_block = CanonicalPiBlock(self.P, self.lr, self.betas, self.eps)
         else:
             const = kappa_sum(x64, math.log(lam_f)) + eta.dirichlet_normaliser(dirichlet_mode)

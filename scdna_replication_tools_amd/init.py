@@ -24,12 +24,19 @@ def _median15(rng: np.random.Generator, ppf, shape):
     return np.median(ppf(u), axis=0)
 
 
-def init_params(kind: int, reads: np.ndarray, libs: np.ndarray, n_libs: int, P: int, K: int, *,
+def init_params(kind: int, reads: Optional[np.ndarray], libs: np.ndarray, n_libs: int, P: int, K: int, *,
                 ploidy: Optional[np.ndarray] = None, t_init: Optional[np.ndarray] = None,
-                beta_means: Optional[np.ndarray] = None, seed: int = 0, method: str = "sampled"
+                beta_means: Optional[np.ndarray] = None, seed: int = 0, method: str = "sampled",
+                mean_reads: Optional[np.ndarray] = None, n_bins: Optional[int] = None
                 ) -> Dict[str, np.ndarray]:
-    """Constrained initial site values (float64) keyed by the reference's site names."""
-    L, N = reads.shape
+    """Constrained initial site values (float64) keyed by the reference's site names.
+    ``reads`` (L, N) may be replaced by its per-cell means ``mean_reads`` (N,) and ``n_bins``
+    (the values are the same; step 1's doubled cells need not be materialised)."""
+    if mean_reads is None:
+        L, N = reads.shape
+        mean_reads = reads.astype(np.float64).mean(0)
+    else:
+        L, N = int(n_bins), int(np.asarray(mean_reads).shape[0])
     K1 = K + 1
     rng = np.random.default_rng(seed)
     sampled = method == "sampled"
@@ -51,7 +58,7 @@ def init_params(kind: int, reads: np.ndarray, libs: np.ndarray, n_libs: int, P: 
     else:
         tau = np.asarray(t_init, dtype=np.float64)
     out["expose_tau"] = tau
-    mu = reads.astype(np.float64).mean(0) / ((1 + tau) * np.asarray(ploidy, dtype=np.float64))
+    mu = np.asarray(mean_reads, dtype=np.float64) / ((1 + tau) * np.asarray(ploidy, dtype=np.float64))
     out["expose_u"] = (mu + (mu / 10.0) * _median15(rng, stats.norm.ppf, (N,))) if sampled else mu
     bm = out["expose_beta_means"] if kind == 1 else np.asarray(beta_means, dtype=np.float64).reshape(n_libs, K1)
     bs = out["expose_beta_stds"]

@@ -32,6 +32,7 @@ from __future__ import annotations
 import contextlib
 import logging
 import os
+import sys
 import time
 from typing import List, Optional
 
@@ -393,6 +394,19 @@ class pert_infer_scRT():
                          dirichlet_mode=self.dirichlet_mode, is_root=dd.rank == 0, n_cells_total=N,
                          allreduce=dd.allreduce, **kw)
 
+    def _shard_pairs(self, dd: _Dist, reads_g, states_g, libs2, init):
+        """Step 1's PertShard in pair mode over this rank's contiguous range of G1/2 cells:
+        both copies of each of its cells (the copies of a cell never straddle ranks)."""
+        NG = reads_g.shape[1]
+        a, b = dd.bounds(NG)
+        idx = np.r_[a:b, NG + a:NG + b]
+        cells = {k: (np.asarray(v)[idx] if k in ("expose_tau", "expose_u", "expose_betas") else v)
+                 for k, v in init.items()}
+        return PertShard(KIND_STEP1, np.ascontiguousarray(reads_g[:, a:b]), self._inp.gc, np.asarray(libs2)[idx],
+                         self.L, self.P, self.K, cells, cn_obs=np.ascontiguousarray(states_g[:, a:b]), paired=True,
+                         device=self.device, lr=self.learning_rate, dirichlet_mode=self.dirichlet_mode,
+                         is_root=dd.rank == 0, n_cells_total=2 * NG, allreduce=dd.allreduce)
+
     def _decode(self, shard: PertShard, dd: _Dist):
         cn, rep = shard.decode()
         c = shard.constrained()
@@ -414,6 +428,11 @@ class pert_infer_scRT():
         # initialisation -- device parts on a side stream
         from concurrent.futures import ThreadPoolExecutor
         helper = ThreadPoolExecutor(max_workers=1, thread_name_prefix="pert-prep")
+        # the fit thread queues launches ahead of the device and gives up the GIL only while it
+        # waits on the device; a helper thread running Python would otherwise keep it for the
+        # interpreter's default 5 ms switch interval, longer than the queue of steps lasts
+        switch = sys.getswitchinterval()
+        sys.setswitchinterval(min(switch, 5e-4))
 
         def on_device(fn, *a):
             # the HIP runtime's current device is per thread: the helper uses the fit's device
@@ -449,14 +468,19 @@ class pert_infer_scRT():
                     t_init, _, _ = self._guess_times(inp.reads_s, etas.argmax_states())
                     if stream is not None:
                         stream.synchronize()
+                self.timings["tau_init_s"] = dict(getattr(guess_times_batched, "last_timings", {}))
                 return profiles, etas, t_init, (t_cons + t1 - t0, time.perf_counter() - t1)
 
             fut_priors = helper.submit(on_device, priors)
 
             # ---- step 1: G1/2 cells doubled, cn / rep observed (:718-774)
-            st_g2, rd_g2, lb_g2, rep_g2 = prep.make_g1_g2_training_data(inp.states_g, inp.reads_g, inp.libs_g)
-            init1 = init_params(KIND_STEP1, rd_g2, lb_g2, n_libs, P, K, seed=self.seed, method=self.init_method)
-            s1 = self._shard(KIND_STEP1, dd, rd_g2, lb_g2, init1, cn_obs=st_g2, rep_obs=rep_g2)
+            # the doubled training set (make_g1_g2_training_data, :228-251) in pair mode: the
+            # G1/2 columns stored once, rep 0 / rep 1 copies as cells [0, NG) / [NG, 2 NG)
+            mean_g = inp.reads_g.astype(np.float64).mean(0)
+            lb_g2 = np.concatenate([inp.libs_g, inp.libs_g])
+            init1 = init_params(KIND_STEP1, None, lb_g2, n_libs, P, K, seed=self.seed, method=self.init_method,
+                                mean_reads=np.concatenate([mean_g, mean_g]), n_bins=inp.reads_g.shape[0])
+            s1 = self._shard_pairs(dd, inp.reads_g, inp.states_g, lb_g2, init1)
             logging.info('STEP 1: Learning reads to CN bias from low variance cells.')
             losses_g = self._svi(s1, self.max_iter_step1, self.min_iter_step1, "step1")
             c1 = s1.constrained()
@@ -517,6 +541,7 @@ class pert_infer_scRT():
         finally:
             # also when a fit or a helper task raised: no helper work outlives the call
             helper.shutdown(wait=True, cancel_futures=True)
+            sys.setswitchinterval(switch)
         self.timings["total"] = time.perf_counter() - t_all
         return cn_s_out, supp_s_out_df, cn_g1_out, supp_g1_out_df
 
@@ -531,6 +556,7 @@ class pert_infer_scRT():
             t_init2, _, _ = self._guess_times(inp.reads_g, etas2.argmax_states())
             if stream is not None:
                 stream.synchronize()
+            self.timings["tau_init_g"] = dict(getattr(guess_times_batched, "last_timings", {}))
         return etas2, t_init2
 
     # ------------------------------------------------------------------ outputs

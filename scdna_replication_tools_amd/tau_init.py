@@ -38,9 +38,14 @@ exact path against sklearn and the whole against prep.guess_times, up to 5,451 b
 from __future__ import annotations
 
 import os
+import time
 
 import numpy as np
 import torch
+# the per-cell reference path's modules, imported with this one (as pert_model.py:18-20
+# imports them): the exact host path calls them
+from scipy.stats import skew
+from sklearn.cluster._kmeans import _kmeans_single_lloyd, _tolerance
 
 MEAN_GAP_THRESH = 0.7
 EARLY_S_SKEW_THRESH = 0.2
@@ -54,7 +59,7 @@ FRAGILE = 1e-5          # relative: mean-gap / skew thresholds
 PP_MARGIN = 2e-6        # relative to the k-means++ potential: candidate draw and choice
 TIE = 1e-6              # relative width of an exact tie on a k-means decision
 EM_MARGIN = 2e-6        # absolute: the EM lower-bound change around its tolerance
-MINOR_EXACT_MAX_L = 2000  # up to this many bins, the finer near-ties are recomputed too
+SYNC_EVERY = 4            # batched loops: iterations between host checks for the end
 
 
 EPS32 = float(np.finfo(np.float32).eps)
@@ -131,7 +136,7 @@ def _lloyd(X: torch.Tensor, centers: torch.Tensor, tol: torch.Tensor, max_iter: 
     c = centers.clone()
     if fragile is None:
         fragile = torch.zeros(N, dtype=torch.bool, device=X.device)
-    for _ in range(max_iter):
+    for it in range(max_iter):
         # pairwise distance as sklearn's chunked kernel ranks it: ||c||^2 - 2 x c
         lab = _assign(X, c, tie_bias)
         w1 = lab.sum(0).to(X.dtype)
@@ -147,7 +152,9 @@ def _lloyd(X: torch.Tensor, centers: torch.Tensor, tol: torch.Tensor, max_iter: 
         labels_old = torch.where(active[None, :], lab, labels_old)
         strict |= active & same
         active &= ~same & ~(shift <= tol)
-        if not bool(active.any()):
+        # (finished columns are masked, so iterations past the last one change nothing: the
+        # host checks for the end every SYNC_EVERY iterations, not after every one)
+        if it % SYNC_EVERY == SYNC_EVERY - 1 and not bool(active.any()):
             break
     final = _assign(X, c, tie_bias)
     return torch.where(strict[None, :], labels_old, final).bool()
@@ -172,7 +179,7 @@ def _gmm_means(X: torch.Tensor, lab1: torch.Tensor, max_iter: int = 100, tol: fl
     lb = torch.full((N,), -float("inf"), dtype=X.dtype, device=X.device)
     active = torch.ones(N, dtype=torch.bool, device=X.device)
     log2pi = float(np.log(2 * np.pi))
-    for _ in range(max_iter):
+    for it in range(max_iter):
         prec = var.rsqrt()
         y = (X[None] - mu[:, None, :]) * prec[:, None, :]
         wlp = -0.5 * (log2pi + y * y) + torch.log(prec)[:, None, :] + torch.log(w)[:, None, :]
@@ -188,7 +195,7 @@ def _gmm_means(X: torch.Tensor, lab1: torch.Tensor, max_iter: int = 100, tol: fl
             fragile |= active & ((change.abs() - tol).abs() <= EM_MARGIN)
         lb = torch.where(active, lb2, lb)
         active &= ~(change.abs() < tol)
-        if not bool(active.any()):
+        if it % SYNC_EVERY == SYNC_EVERY - 1 and not bool(active.any()):
             break
     return mu
 
@@ -368,7 +375,6 @@ def exact_kmeans_labels(x: np.ndarray) -> np.ndarray:
     with the same RandomState draws, distances and BLAS products), then sklearn's own Lloyd
     (``_kmeans_single_lloyd``, on one OpenMP thread: the reference's thread count only
     changes the last bits of the centre sums, never a label short of an exact tie)."""
-    from sklearn.cluster._kmeans import _kmeans_single_lloyd, _tolerance
     X = np.array(x, dtype=F32, order="C").reshape(-1, 1)
     n = X.shape[0]
     tol = _tolerance(X, 1e-4)
@@ -497,7 +503,6 @@ def exact_scan(x: np.ndarray, mean_0, mean_1, MEAN_GAP=MEAN_GAP_THRESH, EARLY=EA
     fraction.  The 100 distances are evaluated in fp64 from sorted prefix sums; only the
     thresholds within SCAN_SLACK of the least are summed the reference's way (fp32
     ``abs(X - B).sum()``; its error is < 1e-5 of the sum), which decides among them."""
-    from scipy.stats import skew
     X = np.asarray(x, dtype=F32).reshape(-1)
     L = X.size
     mean_gap = abs(mean_0 - mean_1)
@@ -581,6 +586,7 @@ def guess_times_batched(reads: np.ndarray, cn_states: np.ndarray, upsilon: float
     change; the others take the exact host path (exact_fractions) -- with the batched
     k-means labels where the partition is certain, else with sklearn's own k-means -- so
     every cell's t_init is the reference's.  No worker processes."""
+    t0 = time.perf_counter()
     dev = torch.device(device) if device is not None else torch.device("cpu")
     x = torch.as_tensor(np.asarray(reads, np.float32))
     st = torch.as_tensor(np.asarray(cn_states, np.float32))
@@ -590,6 +596,7 @@ def guess_times_batched(reads: np.ndarray, cn_states: np.ndarray, upsilon: float
     frac, lab_unsure, near, lab = binarization_fraction(norm.to(dev), return_fragile=True, return_minor=True)
     t = frac.to(torch.float32).cpu().numpy()
     redo = np.flatnonzero((lab_unsure | near).cpu().numpy())
+    t1 = time.perf_counter()
     if redo.size:
         sel = torch.as_tensor(redo, device=lab.device)
         labels = lab[:, sel].T.to(torch.int8).cpu().numpy()
@@ -601,5 +608,8 @@ def guess_times_batched(reads: np.ndarray, cn_states: np.ndarray, upsilon: float
     else:
         guess_times_batched.last_kmeans = 0
     guess_times_batched.last_fragile = redo
+    guess_times_batched.last_timings = {"batched_s": t1 - t0, "exact_s": time.perf_counter() - t1,
+                                        "cells": int(x.shape[1]), "exact_cells": int(redo.size),
+                                        "kmeans_cells": guess_times_batched.last_kmeans}
     alpha = (t * np.float32(upsilon)).astype(np.float32)
     return t, alpha, (np.float32(upsilon) - alpha).astype(np.float32)

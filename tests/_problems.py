@@ -14,7 +14,7 @@ from oracle import pert_oracle as po
 from scdna_replication_tools_amd.engine import EtaCodebook
 from scdna_replication_tools_amd.simulator import simulate
 
-KIND_OF = {"step1": 1, "step2": 2, "step3": 3}
+KIND_OF = {"step1": 1, "step2": 2, "step3": 3, "step1p": 1}     # step1p: step 1 in pair mode
 
 
 def composite_etas(states_a, states_b, P, rng):
@@ -34,9 +34,14 @@ def composite_etas(states_a, states_b, P, rng):
 
 def make_problem(kind: str, L: int = 40, N: int = 70, P: int = 13, K: int = 4, n_libs: int = 2,
                  seed: int = 0, prior: str = "clone", z_scale: float = 1.0, low_reads: bool = False,
-                 reads_fn=None, num_reads=None, subdivide: int = 1):
+                 reads_fn=None, num_reads=None, subdivide: int = 1, pair: bool = False):
     """``L`` bins of the 500 kb grid (or of its ``subdivide``-fold split), ``N`` cells;
-    ``num_reads`` per cell (default: a deep 20x coverage of the 500 kb scDNA regime)."""
+    ``num_reads`` per cell (default: a deep 20x coverage of the 500 kb scDNA regime).
+    ``pair`` (step 1): the product's training set, N / 2 G1/2 cells doubled with rep 0 / 1
+    (pert_model.py:228-251) -- the oracle gets the doubled arrays, PertShard the stored
+    half in pair mode (also ``kind="step1p"``)."""
+    if kind == "step1p":
+        kind, pair = "step1", True
     rng = np.random.default_rng(seed)
     if num_reads is None:
         num_reads = 2e4 if low_reads else 1e6 * L / 5451 * 20
@@ -58,7 +63,15 @@ def make_problem(kind: str, L: int = 40, N: int = 70, P: int = 13, K: int = 4, n
     if kind == "step1":
         rep = np.zeros((L, N))
         rep[:, N // 2:] = 1.0
-        kw.update(cn_obs=states, rep_obs=rep)
+        if pair:
+            assert N % 2 == 0
+            half = N // 2
+            reads = np.concatenate([reads[:, :half], reads[:, :half]], axis=1)
+            states = np.concatenate([states[:, :half], states[:, :half]], axis=1)
+            kw.update(reads=reads[:, :half], cn_obs=states[:, :half], paired=True)
+            op.update(reads=t64(reads))
+        else:
+            kw.update(cn_obs=states, rep_obs=rep)
         op.update(cn_obs=t64(states), rep_obs=t64(rep))
     else:
         if prior == "clone":
@@ -117,5 +130,5 @@ def make_problem(kind: str, L: int = 40, N: int = 70, P: int = 13, K: int = 4, n
 
 def init_constrained(kind: str, z):
     """Constrained values of z for PertShard(init=...)."""
-    c = po.constrain(kind, z)
+    c = po.constrain("step1" if kind == "step1p" else kind, z)
     return {k: v.detach().numpy() for k, v in c.items()}

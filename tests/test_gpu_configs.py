@@ -43,7 +43,7 @@ def _parity(case, kind, prob, kw, z):
     rep = {}
     entry = {"kind": kind, "shape": list(prob.reads.shape), "loss_rel": abs(loss - float(ref_loss)) / abs(float(ref_loss)),
              "sites": rep}
-    skip = ("expose_pi",) if kind == "step1" else ()          # step-1 pi: the canonical block
+    skip = ("expose_pi",) if kind.startswith("step1") else ()          # step-1 pi: the canonical block
     try:
         _bounds.check_all(prob, z, g, ref_g, skip=skip, report=rep)
     finally:
@@ -59,7 +59,7 @@ def test_c3_c4_full_genome_shard_step2(prior):
     _parity("c3c4_shard_step2_" + prior, "step2", prob, kw, z)
 
 
-@pytest.mark.parametrize("kind", ["step1", "step3"])
+@pytest.mark.parametrize("kind", ["step1", "step1p", "step3"])
 def test_c3_c4_full_genome_shard_steps_1_3(kind):
     prob, kw, z = make_problem(kind, L=5451, N=64, num_reads=1e6, seed=23)
     _parity("c3c4_shard_" + kind, kind, prob, kw, z)

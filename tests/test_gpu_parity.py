@@ -38,7 +38,9 @@ def _rel(a, b):
 CASES = [("step2", "clone", 13, 2), ("step2", "composite", 13, 2), ("step3", "clone", 13, 2),
          ("step1", "clone", 13, 2), ("step2", "clone", 12, 2), ("step2", "clone", 5, 2),
          # more libraries than finalize's round-1 slot table held (n_libs * (K+1) > 31)
-         ("step2", "clone", 13, 8), ("step1", "clone", 13, 8)]
+         ("step2", "clone", 13, 8), ("step1", "clone", 13, 8),
+         # step 1 in pair mode (the product's layout of the doubled G1/2 cells)
+         ("step1p", "clone", 13, 2), ("step1p", "clone", 13, 8)]
 
 
 @pytest.mark.parametrize("variant", [0, 3])
@@ -49,7 +51,7 @@ def test_loss_and_grads_match_oracle(kind, prior, P, n_libs, variant):
     sh = _shard(kind, kw, z, variant=variant)
     loss, g = sh.loss_and_grads()
     assert abs(loss - float(ref_loss)) <= LOSS_RTOL * abs(float(ref_loss)), (loss, float(ref_loss))
-    skip = ("expose_pi",) if kind == "step1" else ()   # step-1 pi is the canonical block (test_oracle)
+    skip = ("expose_pi",) if kind.startswith("step1") else ()   # step-1 pi is the canonical block (test_oracle)
     _bounds.check_all(prob, z, g, ref_g, skip=skip)
     for name, gref in ref_g.items():                   # and the round-1 tensor-level bound
         if name not in skip:
@@ -86,7 +88,7 @@ def test_torch32_loss_mode_reports_the_reference_fp32_constant(prior):
 
 
 @pytest.mark.parametrize("variant", [0, 3])
-@pytest.mark.parametrize("kind", ["step2", "step3", "step1"])
+@pytest.mark.parametrize("kind", ["step2", "step3", "step1", "step1p"])
 def test_adam_trajectory(kind, variant):
     """Three SVI steps: losses and every parameter after the updates."""
     prob, kw, z = make_problem(kind, seed=7)
@@ -94,12 +96,12 @@ def test_adam_trajectory(kind, variant):
     sh = _shard(kind, kw, z, variant=variant)
     losses = [sh.step() for _ in range(3)]
     np.testing.assert_allclose(losses, res.losses, rtol=2e-5)
-    c_ref = po.constrain(kind, res.z)
+    c_ref = po.constrain(prob.kind, res.z)
     c_dev = sh.constrained()
     for name, v in c_dev.items():
         ref = c_ref[name].detach().numpy().reshape(np.shape(v))
         np.testing.assert_allclose(v, ref, rtol=2e-4, atol=2e-5, err_msg=name)
-    if kind != "step1":
+    if not kind.startswith("step1"):
         pi_dev = sh.pi().cpu().numpy()
         np.testing.assert_allclose(pi_dev, c_ref["expose_pi"].numpy(), rtol=2e-3, atol=1e-6)
 

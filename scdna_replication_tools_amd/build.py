@@ -81,12 +81,46 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return OUT
 
 
+HOST_SOURCES = [os.path.join(HERE, "csrc", "pert_host.c")]
+HOST_OUT = os.path.join(HERE, "libpert_host.so")
+# no contraction into fma, no reassociation: the helper repeats numpy's fp32 operations exactly
+HOST_FLAGS = ["-O2", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math", "-std=c99"]
+
+
+def host_source_hash() -> str:
+    h = hashlib.sha256()
+    for d in HOST_SOURCES:
+        with open(d, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(HOST_FLAGS).encode())
+    return h.hexdigest()[:HASH_LEN]
+
+
+def build_host(force: bool = False) -> str:
+    """libpert_host.so (gcc): the CPU helpers of tau_init's exact path.  Rebuilt when the
+    hash of its sources (kept in a stamp file beside it) changes."""
+    stamp = HOST_OUT + ".src"
+    want = host_source_hash()
+    if not force and os.path.exists(HOST_OUT) and os.path.exists(stamp) and open(stamp).read().strip() == want:
+        return HOST_OUT
+    cmd = [os.environ.get("CC", "gcc"), *HOST_FLAGS, *HOST_SOURCES, "-o", HOST_OUT + ".tmp"]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        sys.stderr.write(res.stdout + res.stderr)
+        raise RuntimeError("gcc failed building {}".format(HOST_OUT))
+    os.replace(HOST_OUT + ".tmp", HOST_OUT)
+    with open(stamp, "w") as fh:
+        fh.write(want)
+    return HOST_OUT
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args()
     print(build(force=a.force, verbose=a.verbose))
+    print(build_host(force=a.force))
 
 
 if __name__ == "__main__":

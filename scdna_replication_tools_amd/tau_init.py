@@ -417,6 +417,88 @@ def _lse2(a: np.ndarray) -> np.ndarray:
     return out
 
 
+class _HostHelper:
+    """libpert_host.so (csrc/pert_host.c: the EM's M step and lower bound over all bins, the
+    GIL released) bound to numpy's own BLAS (the cblas_sgemv / cblas_sdot numpy calls for
+    ``np.dot``).  ``get()`` is None when either is not available; the numpy restatement then
+    runs the same operations (same results, slower)."""
+    _inst = False
+
+    @classmethod
+    def get(cls):
+        if cls._inst is False:
+            cls._inst = cls._load()
+        return cls._inst
+
+    @staticmethod
+    def _load():
+        import ctypes
+        from ctypes import POINTER, c_float, c_int64, c_void_p
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpert_host.so")
+        blas = _numpy_blas()
+        if blas is None or not os.path.exists(path):
+            return None
+        try:
+            lib = ctypes.CDLL(path)                       # CDLL: the calls release the GIL
+        except OSError:
+            return None
+        f = lib.pert_host_em_mstep
+        fp = POINTER(c_float)
+        f.argtypes = [c_int64, c_int64, c_int64, POINTER(c_int64), fp, fp, POINTER(c_int64), fp, c_void_p, c_void_p,
+                      fp, fp, fp, fp, fp]
+        f.restype = ctypes.c_int
+        lib.pert_host_pairwise_sum.argtypes = [fp, c_int64]
+        lib.pert_host_pairwise_sum.restype = c_float
+        h = _HostHelper()
+        h.lib, h.sgemv, h.sdot = lib, blas[0], blas[1]
+        return h
+
+    def mstep(self, rows, resp_u, lpn_u, inv, X):
+        """(nk, means, cov + reg_covar, lb) of the cells ``rows`` (see pert_host.c)."""
+        import ctypes
+        from ctypes import POINTER, c_float, c_int64
+        m, U = resp_u.shape[0], resp_u.shape[1]
+        L = X.shape[1]
+        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        resp_u = np.ascontiguousarray(resp_u, dtype=F32)
+        nk, means, cov = (np.empty((m, 2), F32) for _ in range(3))
+        lb = np.empty(m, F32)
+        scratch = np.empty(4 * L, F32)
+        fp = lambda a: a.ctypes.data_as(POINTER(c_float))
+        lp = None
+        if lpn_u is not None:
+            lpn_u = np.ascontiguousarray(lpn_u, dtype=F32)
+            lp = fp(lpn_u)
+        self.lib.pert_host_em_mstep(m, L, U, rows.ctypes.data_as(POINTER(c_int64)), fp(resp_u), lp,
+                                    inv.ctypes.data_as(POINTER(c_int64)), fp(X), self.sgemv, self.sdot,
+                                    fp(nk), fp(means), fp(cov), fp(lb), fp(scratch))
+        return nk, means, cov, lb
+
+
+def _numpy_blas():
+    """Addresses of cblas_sgemv / cblas_sdot in the BLAS numpy itself calls (its bundled
+    scipy-openblas, ILP64 interface), or None."""
+    import ctypes
+    try:
+        from threadpoolctl import threadpool_info
+        libs = [d for d in threadpool_info() if d.get("user_api") == "blas" and "numpy" in d.get("filepath", "")]
+    except Exception:                                     # noqa: BLE001  (no threadpoolctl / odd layout)
+        return None
+    for d in libs:
+        try:
+            h = ctypes.CDLL(d["filepath"])
+        except OSError:
+            continue
+        for pre, suf in (("scipy_", "64_"), ("", "64_")):
+            try:
+                g = getattr(h, pre + "cblas_sgemv" + suf)
+                s = getattr(h, pre + "cblas_sdot" + suf)
+            except AttributeError:
+                continue
+            return ctypes.cast(g, ctypes.c_void_p).value, ctypes.cast(s, ctypes.c_void_p).value
+    return None
+
+
 def _distinct(Xs: np.ndarray):
     """Per row of Xs (n, L): the sorted distinct values, their counts and the inverse map."""
     n, L = Xs.shape
@@ -430,7 +512,7 @@ def _distinct(Xs: np.ndarray):
 
 
 def exact_gmm_means(Xs: np.ndarray, labels: np.ndarray, max_iter: int = 100, tol: float = 1e-3,
-                    distinct=None) -> np.ndarray:
+                    distinct=None, use_host: bool = True) -> np.ndarray:
     """``GaussianMixture(n_components=2, random_state=0).fit_predict(X).means_`` for every
     row X of Xs (n, L) fp32, from the k-means ``labels`` (n, L): sklearn's EM
     (mixture/_base.py fit_predict; _gaussian_mixture.py _initialize, _m_step,
@@ -440,17 +522,28 @@ def exact_gmm_means(Xs: np.ndarray, labels: np.ndarray, max_iter: int = 100, tol
     ``resp.sum(axis=0)`` (numpy adds the rows in order, i.e. a cumulative sum), and per cell
     the BLAS calls sklearn makes -- ``np.dot(resp.T, X)`` (gemv on an (L, 2) C-ordered
     array) and ``np.dot(resp[:, k] * diff.T, diff)`` (sdot of two contiguous vectors); the
-    1x1 Cholesky factor and triangular solve are sqrt and 1 / l.  Returns (n, 2) fp32."""
+    1x1 Cholesky factor and triangular solve are sqrt and 1 / l.  The M step runs in
+    libpert_host.so when it and numpy's BLAS are found (``use_host``), else in numpy: the
+    same operations either way.  Returns (n, 2) fp32."""
     n, L = Xs.shape
-    xs = [np.array(Xs[i], dtype=F32).reshape(L, 1) for i in range(n)]
+    Xs = np.ascontiguousarray(Xs, dtype=F32)
+    host = _HostHelper.get() if use_host else None
+    xs = [np.array(Xs[i], dtype=F32).reshape(L, 1) for i in range(n)] if host is None else None
     uniq, _, inv = _distinct(Xs) if distinct is None else distinct
+    inv = np.ascontiguousarray(inv, dtype=np.int64)
     U = max(len(u) for u in uniq)
     Xu = np.empty((n, U), F32)
     for i, u in enumerate(uniq):
         Xu[i, :len(u)] = u
         Xu[i, len(u):] = u[0]
-    resp = np.zeros((n, L, 2), dtype=F32)
-    resp[np.arange(n)[:, None], np.arange(L)[None, :], np.asarray(labels, np.intp)] = 1
+    if host is not None:
+        # the initial M step through the helper: "distinct values" = the two labels
+        lab = np.ascontiguousarray(labels, dtype=np.int64)
+        onehot = np.broadcast_to(np.eye(2, dtype=F32)[None], (n, 2, 2))
+        w, means, cov, _ = host.mstep(np.arange(n), onehot, None, lab, Xs)
+    else:
+        resp = np.zeros((n, L, 2), dtype=F32)
+        resp[np.arange(n)[:, None], np.arange(L)[None, :], np.asarray(labels, np.intp)] = 1
 
     def mstep(resp, rows):
         m = len(rows)
@@ -467,7 +560,8 @@ def exact_gmm_means(Xs: np.ndarray, labels: np.ndarray, max_iter: int = 100, tol
             cov[j, 1] = np.dot(prod[j, 1], diff[j, 1])
         return nk, means, cov / nk + 1e-6
 
-    w, means, cov = mstep(resp, np.arange(n))
+    if host is None:
+        w, means, cov = mstep(resp, np.arange(n))
     w = w / L
     pc = F32(1) / np.sqrt(cov)
     lower = np.full(n, -np.inf, dtype=F32)
@@ -480,10 +574,13 @@ def exact_gmm_means(Xs: np.ndarray, labels: np.ndarray, max_iter: int = 100, tol
         lpn_u = _lse2(wlp)
         with np.errstate(under="ignore"):
             resp_u = np.exp(wlp - lpn_u[:, :, None])
-        ia = inv[a] + (np.arange(len(a)) * U)[:, None]       # flat gather of the distinct values
-        lb = np.mean(np.take(lpn_u, ia), axis=1)
-        ia2 = 2 * ia
-        w2, m2, c2 = mstep(np.take(resp_u, np.stack([ia2, ia2 + 1], axis=2)), a)
+        if host is not None:
+            w2, m2, c2, lb = host.mstep(a, resp_u, lpn_u, inv, Xs)
+        else:
+            ia = inv[a] + (np.arange(len(a)) * U)[:, None]   # flat gather of the distinct values
+            lb = np.mean(np.take(lpn_u, ia), axis=1)
+            ia2 = 2 * ia
+            w2, m2, c2 = mstep(np.take(resp_u, np.stack([ia2, ia2 + 1], axis=2)), a)
         w[a] = w2 / (w2[:, :1] + w2[:, 1:])
         means[a], cov[a] = m2, c2
         pc[a] = F32(1) / np.sqrt(c2)

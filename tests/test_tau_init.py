@@ -132,3 +132,22 @@ def test_no_worker_processes_in_the_product_path():
         src = inspect.getsource(mod)
         for word in ("joblib", "loky", "multiprocessing", "ProcessPool"):
             assert word not in src, (mod.__name__, word)
+
+
+def test_host_helper_equals_numpy_restatement():
+    """libpert_host.so's M step (numpy's BLAS, numpy's reduction orders, no GIL) gives the
+    numpy restatement's GMM means bit for bit; its pairwise sum is numpy's float32 sum."""
+    import ctypes
+    host = tau_init._HostHelper.get()
+    assert host is not None, "libpert_host.so or numpy's BLAS not found"
+    rng = np.random.default_rng(2)
+    for n in (1, 7, 8, 127, 128, 129, 1000, 5451, 6000):
+        a = (rng.standard_normal(n) * 10.0 ** rng.uniform(-3, 3, n)).astype(np.float32)
+        got = host.lib.pert_host_pairwise_sum(a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n)
+        assert np.float32(got) == np.sum(a), n
+    reads, states = _profiles(n_s=40, n_g=8, L=5451, seed=13)
+    norm = _norm(reads, states)
+    Xs = tau_init.standardize_rows(norm.T)
+    labs = np.stack([tau_init.exact_kmeans_labels(Xs[j]) for j in range(Xs.shape[0])])
+    np.testing.assert_array_equal(tau_init.exact_gmm_means(Xs, labs, use_host=True),
+                                  tau_init.exact_gmm_means(Xs, labs, use_host=False))

@@ -575,9 +575,9 @@ class pert_infer_scRT():
         keys = getattr(cn_s_reads_df, "keys", None)
         if keys is not None and not isinstance(keys, prep.TableKeys):
             keys = None                                   # a DataFrame's .keys is a method
-        if keys is not None and len(keys.cell_code) == len(cn_s) and keys.is_grid(cells, loci_chr, loci_start):
+        if keys is not None and prep._n_rows(keys) == len(cn_s) and keys.is_grid(cells, loci_chr, loci_start):
             ci = li = None                                # row i = (cell i // L, locus i % L)
-        elif keys is not None and len(keys.cell_code) == len(cn_s):
+        elif keys is not None and prep._n_rows(keys) == len(cn_s):
             ci, li = keys.row_positions(cells, loci_chr, loci_start)
         else:
             cell_index = pd.Index(cells.astype(str))

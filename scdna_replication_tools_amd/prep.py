@@ -272,6 +272,129 @@ class TableKeys:
         return ci, li
 
 
+class RegularKeys(TableKeys):
+    """TableKeys of a sorted regular table (row i = cell i // L, locus i % L, every key
+    valid): the per-row code arrays are made only when a consumer asks for them."""
+
+    def __init__(self, cells, loci_chr, loci_start, L: int):
+        self.cells = np.asarray(cells)
+        self.loci_chr = np.asarray(loci_chr, dtype=object)
+        self.loci_start = np.asarray(loci_start)
+        self.regular = int(L)
+        self._cc = self._lc = None
+
+    @property
+    def n_rows(self) -> int:
+        return self.cells.size * self.regular
+
+    @property
+    def cell_code(self):
+        if self._cc is None:
+            self._cc = np.repeat(np.arange(self.cells.size, dtype=np.int64), self.regular)
+        return self._cc
+
+    @property
+    def locus_code(self):
+        if self._lc is None:
+            self._lc = np.tile(np.arange(self.regular, dtype=np.int64), self.cells.size)
+        return self._lc
+
+    @property
+    def valid(self):
+        return np.ones(self.n_rows, dtype=bool)
+
+
+def _n_rows(keys) -> int:
+    return keys.n_rows if isinstance(keys, RegularKeys) else len(keys.cell_code)
+
+
+def _same_objects(a: np.ndarray, B: int, L: int) -> bool:
+    """Every (B, L) row of the object column ``a`` holds the values of its first row: by
+    object identity first, values compared only where the objects differ."""
+    a = np.ascontiguousarray(a)
+    if a.dtype != object:
+        a2 = a.reshape(B, L)
+        return bool((a2 == a2[:1]).all())
+    p2 = _object_pointers(a).reshape(B, L)
+    diff = p2 != p2[:1]
+    if not diff.any():
+        return True
+    if diff.sum() * 16 > a.size:
+        return False                                   # mostly distinct objects: the general path
+    a2 = a.reshape(B, L)
+    return bool((a2[diff] == np.broadcast_to(a2[:1], (B, L))[diff]).all())
+
+
+def _constant_rows(a: np.ndarray, B: int, L: int) -> bool:
+    """Every (B, L) row of ``a`` holds one value (object identity first, as _same_objects)."""
+    a = np.ascontiguousarray(a)
+    if a.dtype != object:
+        a2 = a.reshape(B, L)
+        return bool((a2 == a2[:, :1]).all())
+    p2 = _object_pointers(a).reshape(B, L)
+    diff = p2 != p2[:, :1]
+    if not diff.any():
+        return True
+    if diff.sum() * 16 > a.size:
+        return False
+    a2 = a.reshape(B, L)
+    return bool((a2[diff] == np.broadcast_to(a2[:, :1], (B, L))[diff]).all())
+
+
+def _block_layout(cn: pd.DataFrame, cell_col: str, chr_col: str, start_col: str, notna_col: Optional[str]):
+    """Per-cell blocks (the per-cell HMMcopy tables concatenated): every cell's rows one
+    contiguous block of L rows, every block the same valid locus sequence (any order, no
+    repeats).  Found from the block heads only -- object identity runs of the cell column, one
+    integer compare of the starts, one identity compare of the chromosome labels -- without
+    hashing any per-row string.  Returns (B, L, bp, q, chr codes of block 0) with ``bp`` the
+    blocks in sorted cell order and ``q`` the loci of a block in (chr, start) order, or None."""
+    cell = np.ascontiguousarray(cn[cell_col].to_numpy())
+    n = cell.size
+    if n == 0 or cell.dtype != object:
+        return None
+    ptr = _object_pointers(cell)
+    d = np.flatnonzero(ptr[1:] != ptr[:-1])
+    if d.size * 16 > n:
+        return None
+    if d.size:
+        d = d[cell[1:][d] != cell[:-1][d]]
+    B = d.size + 1
+    if n % B or B * 16 > n:
+        return None
+    L = n // B
+    if B > 1 and not np.array_equal(d + 1, np.arange(1, B, dtype=d.dtype) * L):
+        return None
+    names = cell[::L]
+    if not all(isinstance(x, str) for x in names) or len(set(names)) != B:
+        return None
+    st = cn[start_col].to_numpy()
+    if st.dtype.kind not in "iu" or (st.size and (st.min() < 0 or st.max() >= (1 << 32))):
+        return None
+    if not _same_objects(st, B, L):
+        return None
+    chc = cn[chr_col]
+    if isinstance(chc.dtype, pd.CategoricalDtype):
+        if not _same_objects(chc.cat.codes.to_numpy(), B, L):
+            return None
+    elif not _same_objects(chc.to_numpy(), B, L):
+        return None
+    ch0 = _chr_codes(chc.iloc[:L])
+    if (ch0 < 0).any():
+        return None
+    if notna_col is not None:
+        v = cn[notna_col].to_numpy()
+        if v.dtype.kind == "f" and np.isnan(v).any():
+            return None
+        if v.dtype == object and pd.isna(v).any():
+            return None
+    lkey0 = ch0.astype(np.int64) << 32 | st[:L].astype(np.int64)
+    q = np.argsort(lkey0, kind="stable")
+    if np.unique(lkey0).size != L:
+        return None                                    # a locus twice in a cell: the general path
+    bp = np.argsort(names, kind="stable")
+    return B, L, bp, q, ch0
+
+
 def pivot_cells_by_loci(cn: pd.DataFrame, value_col: str, cell_col: str, chr_col: str, start_col: str,
                         keys: Optional[TableKeys] = None) -> Pivot:
     """``cn.pivot_table(index=cell, columns=[chr, start], values=col).T`` without the
@@ -280,7 +403,7 @@ def pivot_cells_by_loci(cn: pd.DataFrame, value_col: str, cell_col: str, chr_col
     dropped, cells / loci with no value at all dropped (pivot_table's dropna)."""
     k = TableKeys(cn, cell_col, chr_col, start_col) if keys is None else keys
     val = cn[value_col].to_numpy(np.float64)
-    if getattr(k, "regular", 0) and val.size == k.cell_code.size:
+    if getattr(k, "regular", 0) and val.size == _n_rows(k):
         # one row per (cell, locus) in (cell, locus) order: the pivot is a transpose
         N, L = k.cells.size, k.loci_start.size
         out = np.ascontiguousarray(val.reshape(N, L).T)
@@ -336,10 +459,16 @@ class PertInputs:
 
 
 def _trunc32(a):
-    return np.asarray(a).astype(np.int64).astype(np.float32)
+    a = np.asarray(a)
+    if a.dtype == np.float32:
+        return a                   # a block pivot of an integer column: already the exact values
+    return a.astype(np.int64).astype(np.float32)
 
 
 def _align(p: Pivot, chr_, start) -> Pivot:
+    if (len(p.loci_start) == len(start) and np.array_equal(p.loci_start, start)
+            and np.array_equal(np.asarray(p.loci_chr).astype(str), np.asarray(chr_).astype(str))):
+        return p                                        # already in that locus order
     key = pd.MultiIndex.from_arrays([p.loci_chr, p.loci_start])
     want = pd.MultiIndex.from_arrays([chr_, start])
     idx = key.get_indexer(want)
@@ -350,6 +479,17 @@ def _align(p: Pivot, chr_, start) -> Pivot:
 def _cell_libraries(cn: pd.DataFrame, keys: TableKeys, library_col: str, cells: np.ndarray):
     """(cell, library) pairs of get_libraries_tensor (:206-225) from the integer keys:
     the library labels in first-appearance order and one label per pivot cell."""
+    if isinstance(keys, RegularKeys):
+        # one label per cell block (else the general path below finds and refuses the cell
+        # with two libraries)
+        v = cn[library_col].to_numpy()
+        B, L = keys.cells.size, keys.regular
+        if v.size == B * L and _constant_rows(v, B, L):
+            per_cell = v[::L]                            # one label per sorted cell
+            if not pd.isna(per_cell).any():
+                ids = list(pd.unique(per_cell))          # first appearance over the sorted rows
+                lab = pd.Series(per_cell, index=pd.Index(keys.cells)).reindex(np.asarray(cells)).to_numpy()
+                return ids, lab
     lib_code, lib_uniq = _factorize(cn[library_col].to_numpy())
     cc = keys.cell_code
     fast = False
@@ -387,6 +527,9 @@ def process_input_data(cn_s: pd.DataFrame, cn_g1: pd.DataFrame, input_col="reads
     def table(cn, hook=None):
         # the two tables are independent: sorted and pivoted on two threads (the numpy
         # passes release the GIL; the object-column passes interleave)
+        lay = _block_layout(cn, cell_col, chr_col, start_col, input_col)
+        if lay is not None:
+            return _block_table(cn, lay, hook, input_col, cn_state_col, cell_col, chr_col, start_col)
         cn, k = _sorted_table(cn, cell_col, chr_col, start_col, notna_col=input_col)
         if hook is not None:
             hook(cn, k)
@@ -414,7 +557,7 @@ def process_input_data(cn_s: pd.DataFrame, cn_g1: pd.DataFrame, input_col="reads
 
     # gc per locus: first row of each locus in the sorted S table
     gcv = cn_s[gc_col].to_numpy(np.float64)
-    if getattr(ks, "regular", 0) and gcv.size == ks.cell_code.size:
+    if getattr(ks, "regular", 0) and gcv.size == _n_rows(ks):
         gc_locus = gcv[:ks.regular]                      # regular table: cell 0's rows, locus order
     else:
         okr = ks.valid
@@ -427,13 +570,54 @@ def process_input_data(cn_s: pd.DataFrame, cn_g1: pd.DataFrame, input_col="reads
         raise ValueError("{} is missing for some loci".format(gc_col))
 
     reads_s, reads_g = _trunc32(ps_r.values), _trunc32(pg_r.values)
-    raw = lambda v, t: None if np.array_equal(v, t) else v
+    raw = lambda v, t: None if (v is t or np.array_equal(v, t)) else v
     inp = PertInputs(loci_chr=ps_r.loci_chr, loci_start=ps_r.loci_start, cells_s=ps_r.cells, cells_g=pg_r.cells,
                      reads_s=reads_s, states_s=_trunc32(ps_s.values),
                      reads_g=reads_g, states_g=_trunc32(pg_s.values), gc=gc,
                      libs_s=libs_s, libs_g=libs_g, library_ids=all_ids, keys_s=ks, keys_g=kg,
                      reads_s_raw=raw(ps_r.values, reads_s), reads_g_raw=raw(pg_r.values, reads_g))
     return cn_s, cn_g1, inp
+
+
+def _block_pivot(v: np.ndarray, B: int, L: int, bp: np.ndarray, q: np.ndarray) -> np.ndarray:
+    """The (loci x cells) pivot of a per-cell-block column: (L, B), cells in sorted order
+    (``bp``), loci in (chr, start) order (``q``) -- a transpose of the blocks.  Integer
+    columns whose values fp32 holds exactly come as float32 (the int64-truncated fp32 tensor
+    of pert_model.py:163-166 itself), others as float64."""
+    g = np.asarray(v).reshape(B, L)
+    g = g[bp] if not np.array_equal(bp, np.arange(B)) else g
+    if not np.array_equal(q, np.arange(L)):
+        g = g[:, q]
+    exact32 = g.dtype.kind in "iu" and (g.size == 0 or (g.min() > -(1 << 24) and g.max() < (1 << 24)))
+    out = np.empty((L, B), dtype=np.float32 if exact32 else np.float64)
+    out[...] = g.T
+    return out
+
+
+def _block_table(cn, lay, hook, input_col, cn_state_col, cell_col, chr_col, start_col):
+    """process_input_data's per-table work for a per-cell-block table (_block_layout): the
+    table sorted by (cell, chr, start) with one gather per column (the cell and chromosome
+    columns rebuilt from the block heads), RegularKeys, and the two pivots as transposes of
+    the blocks -- no per-row hashing of the labels."""
+    B, L, bp, q, ch0 = lay
+    cells = np.ascontiguousarray(cn[cell_col].to_numpy())[::L][bp]
+    chq = ch0[q]
+    loci_chr = np.array(CHR_ORDER, dtype=object)[chq]
+    loci_start = cn[start_col].to_numpy()[:L][q]
+    order = (bp.astype(np.int64)[:, None] * L + q[None, :]).reshape(-1)
+    chr_cat = pd.Categorical.from_codes(np.tile(chq.astype(np.int8), B), categories=CHR_ORDER)
+    out = _take_columns(cn, order, replace={cell_col: np.repeat(cells.astype(object), L), chr_col: chr_cat})
+    k = RegularKeys(cells, loci_chr, loci_start, L)
+    if hook is not None:
+        hook(out, k)
+
+    def pivot(col):
+        v = cn[col].to_numpy()
+        if v.dtype.kind == "f" and np.isnan(v).any():
+            # missing values: pivot_table's NaN handling on the sorted table
+            return drop_incomplete_loci(pivot_cells_by_loci(out, col, cell_col, chr_col, start_col, k))
+        return Pivot(cells, loci_chr, loci_start, _block_pivot(v, B, L, bp, q))
+    return out, k, pivot(input_col), pivot(cn_state_col)
 
 
 # --------------------------------------------------------------------------- clones
@@ -558,13 +742,13 @@ def consensus_clone_profiles(cn: pd.DataFrame, col_name: str, clone_col="clone_i
         kc = np.where(kc == bad, -1, kc)
     rows = kc >= 0
     if cn_state_col is not None:
-        if keys is not None and len(keys.cell_code) == len(cn):
+        if keys is not None and _n_rows(keys) == len(cn):
             cc, cells = keys.cell_code, keys.cells
         else:
             cc, cells = _sorted_codes(cn[cell_col].to_numpy())
         cc = np.where(rows, cc, -1)
         rows &= _majority_ploidy_rows(cn, clone_col, cell_col, cn_state_col, cc, len(cells), kc, len(ku))
-    if keys is not None and len(keys.cell_code) == len(cn) and isinstance(cn[chr_col].dtype, pd.CategoricalDtype):
+    if keys is not None and _n_rows(keys) == len(cn) and isinstance(cn[chr_col].dtype, pd.CategoricalDtype):
         # the sorted table's locus codes (sorted (chr category, start) uniques), no re-hashing
         lc = keys.locus_code
         ok = lc >= 0
@@ -594,10 +778,13 @@ def consensus_clone_profiles(cn: pd.DataFrame, col_name: str, clone_col="clone_i
 def first_clone(cn: pd.DataFrame, cells, cell_col="cell_id", clone_col="clone_id", keys=None) -> np.ndarray:
     """cn.loc[cn[cell]==id][clone].values[0] for every id (pert_model.py:289-290).
     ``keys``: the table's TableKeys (row order), to find first rows by cell code."""
-    if keys is not None and len(keys.cell_code) == len(cn):
-        ok = keys.cell_code >= 0
-        _, first = np.unique(keys.cell_code[ok], return_index=True)
-        rows = np.flatnonzero(ok)[first]
+    if keys is not None and _n_rows(keys) == len(cn):
+        if isinstance(keys, RegularKeys):
+            rows = np.arange(keys.cells.size) * keys.regular          # each cell's first row
+        else:
+            ok = keys.cell_code >= 0
+            _, first = np.unique(keys.cell_code[ok], return_index=True)
+            rows = np.flatnonzero(ok)[first]
         clone_of = cn[clone_col].to_numpy()[rows]                  # per keys.cells
         pos = pd.Index(keys.cells).get_indexer(np.asarray(cells))
         out = np.empty(len(pos), dtype=object)

@@ -158,7 +158,7 @@ def to_long_form(sim: SyntheticPERT, input_col: str = "reads", n_libs: int = 1, 
     ``order='bin'``: rows grouped by bin."""
     import pandas as pd
     L = sim.n_bins
-    clone_names = np.array([chr(ord("A") + i) for i in range(sim.clone_cn.shape[1])])
+    clone_names = np.array([chr(ord("A") + i) for i in range(sim.clone_cn.shape[1])], dtype=object)
 
     def frame(reads, cn, clone, prefix, rep=None, tau=None):
         n = reads.shape[1]
@@ -169,8 +169,10 @@ def to_long_form(sim: SyntheticPERT, input_col: str = "reads", n_libs: int = 1, 
             copy = cn.astype(np.float64)
         else:
             raise ValueError(copy_from)
-        cells = np.array(["cell_{}_{}".format(prefix, i) for i in range(n)])
-        libs = np.array(["LIB{}".format(i % n_libs) for i in range(n)])
+        # labels as object arrays: np.repeat then shares one Python string per label, as a table
+        # read with pandas.read_csv holds them (its parser reuses the object of a repeated value)
+        cells = np.array(["cell_{}_{}".format(prefix, i) for i in range(n)], dtype=object)
+        libs = np.array(["LIB{}".format(i % n_libs) for i in range(n)], dtype=object)
         if order == "cell":
             per_bin = lambda a: np.tile(a, n)                 # (L,) bin attribute -> rows
             per_cell = lambda a: np.repeat(a, L)              # (n,) cell attribute -> rows

@@ -42,8 +42,10 @@ def _t(a, dtype):
     return torch.as_tensor(np.asarray(a)).to(dtype)
 
 
-def oracle_chain(m, dtype=torch.float32, t_init_fn=None, log=None) -> dict:
-    """The chained oracle fit of ``m`` (a pert_infer_scRT; only its prep is used)."""
+def oracle_chain(m, dtype=torch.float32, t_init_fn=None, log=None, cell_chunk=None) -> dict:
+    """The chained oracle fit of ``m`` (a pert_infer_scRT; only its prep is used).
+    ``cell_chunk``: evaluate the ELBO and its gradient in cell chunks (the same sums in
+    another order: a second fp32 run of the same algebra)."""
     inp = m._prepare()
     P, K, nl = m.P, m.K, m.L
     profiles = prep.consensus_clone_profiles(m.cn_g1, m.cn_state_col, clone_col=m.clone_col, cell_col=m.cell_col,
@@ -61,7 +63,7 @@ def oracle_chain(m, dtype=torch.float32, t_init_fn=None, log=None) -> dict:
     prob1 = po.OracleProblem("step1", _t(rd_g2, dtype), gc, torch.as_tensor(lb_g2, dtype=torch.long), nl, P, K,
                              cn_obs=_t(st_g2, dtype), rep_obs=_t(rep_g2, dtype))
     r1 = po.fit(prob1, _z0("step1", init1, L, N1, P, dtype), lr=m.learning_rate, max_iter=m.max_iter_step1,
-                min_iter=m.min_iter_step1, rel_tol=m.rel_tol)
+                min_iter=m.min_iter_step1, rel_tol=m.rel_tol, cell_chunk=cell_chunk)
     c1 = po.constrain("step1", r1.z)
     lam = c1["expose_lambda"].detach().to(torch.float32).numpy()
     bm = c1["expose_beta_means"].detach().to(torch.float32).numpy()
@@ -79,7 +81,7 @@ def oracle_chain(m, dtype=torch.float32, t_init_fn=None, log=None) -> dict:
                              P, K, etas=_t(etas.dense(), dtype), lamb=_t(lam, dtype), beta_means=_t(bm, dtype),
                              t_init=_t(t_init, dtype))
     r2 = po.fit(prob2, _z0("step2", init2, L, N2, P, dtype), lr=m.learning_rate, max_iter=m.max_iter,
-                min_iter=m.min_iter, rel_tol=m.rel_tol)
+                min_iter=m.min_iter, rel_tol=m.rel_tol, cell_chunk=cell_chunk)
     c2 = po.constrain("step2", r2.z)
     cn2, rep2 = po.decode(prob2, r2.z)
     out.update(losses_s=np.asarray(r2.losses), t_init_s=t_init, cn_s=cn2.numpy().astype(np.uint8),
@@ -102,7 +104,7 @@ def oracle_chain(m, dtype=torch.float32, t_init_fn=None, log=None) -> dict:
                                  rho_fixed=_t(out["rho"], dtype).reshape(L, 1), a_fixed=_t(out["a"], dtype),
                                  t_init=_t(t_init2, dtype))
         r3 = po.fit(prob3, _z0("step3", init3, L, N3, P, dtype), lr=m.learning_rate, max_iter=m.max_iter_step3,
-                    min_iter=m.min_iter_step3, rel_tol=m.rel_tol)
+                    min_iter=m.min_iter_step3, rel_tol=m.rel_tol, cell_chunk=cell_chunk)
         c3 = po.constrain("step3", r3.z)
         cn3, rep3 = po.decode(prob3, r3.z)
         out.update(losses_s2=np.asarray(r3.losses), t_init_g=t_init2, cn_g=cn3.numpy().astype(np.uint8),

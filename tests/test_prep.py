@@ -12,7 +12,7 @@ CHR = [str(i + 1) for i in range(22)] + ["X", "Y"]
 
 
 def _table(n_cells=7, prefix="c", seed=0, chroms=("1", "2", "10", "X"), per_chr=6, n_libs=2, nan_locus=False,
-           order="shuffled"):
+           order="shuffled", shared=False):
     rng = np.random.default_rng(seed)
     rows = []
     for i in range(n_cells):
@@ -42,6 +42,12 @@ def _table(n_cells=7, prefix="c", seed=0, chroms=("1", "2", "10", "X"), per_chr=
     if nan_locus:                   # one locus missing in one cell: dropped for every cell
         c0 = df.cell_id.iloc[0]
         df.loc[(df.cell_id == c0) & (df.chr == "2") & (df.start == 1), "reads"] = np.nan
+    if shared:
+        # one Python object per distinct label (as np.repeat-built or CSV-parsed tables hold
+        # them): the per-cell block layout is then recognised from object identity
+        for c in ("cell_id", "chr", "library_id", "clone_id"):
+            canon = {}
+            df[c] = pd.Series([canon.setdefault(v, v) for v in df[c].tolist()], dtype=object)
     return df
 
 
@@ -70,21 +76,30 @@ def _ref_process(cn_s, cn_g1):
                 ids=ids, gc=gam["gc"].to_numpy(np.float32))
 
 
+@pytest.mark.parametrize("shared", [False, True])
 @pytest.mark.parametrize("order", ["shuffled", "cells", "cells_split", "cells_unsorted"])
 @pytest.mark.parametrize("nan_locus", [False, True])
-def test_process_input_data_matches_pandas(nan_locus, order):
-    s = _table(9, "s", seed=1, nan_locus=nan_locus, order=order)
-    g = _table(6, "g", seed=2, n_libs=3, nan_locus=nan_locus, order=order)
+def test_process_input_data_matches_pandas(nan_locus, order, shared):
+    s = _table(9, "s", seed=1, nan_locus=nan_locus, order=order, shared=shared)
+    g = _table(6, "g", seed=2, n_libs=3, nan_locus=nan_locus, order=order, shared=shared)
     ref = _ref_process(s, g)
-    blocks = []
-    real = prep._cell_blocks
+    blocks, layouts = [], []
+    real, real_lay = prep._cell_blocks, prep._block_layout
     prep._cell_blocks = lambda *a: blocks.append(real(*a)) or blocks[-1]
+    prep._block_layout = lambda *a: layouts.append(real_lay(*a)) or layouts[-1]
     try:
         cn_s, cn_g1, inp = prep.process_input_data(s, g)
     finally:
-        prep._cell_blocks = real
-    # the per-cell block permutation ran where the table is made of whole per-cell blocks
-    assert [b is not None for b in blocks] == [order in ("cells", "cells_unsorted")] * 2
+        prep._cell_blocks, prep._block_layout = real, real_lay
+    # whole per-cell blocks: recognised from the labels' object identity (the block path,
+    # no per-row hashing) where the labels are shared objects and no read is missing, else
+    # by the per-cell block permutation of the general path
+    per_cell = order in ("cells", "cells_unsorted")
+    fast = per_cell and shared and not nan_locus
+    assert [x is not None for x in layouts] == [fast] * 2
+    assert [b is not None for b in blocks] == ([] if fast else [per_cell] * 2)
+    if fast:
+        assert isinstance(inp.keys_s, prep.RegularKeys) and isinstance(inp.keys_g, prep.RegularKeys)
     # sorted long tables: same rows in the same order, same columns and dtypes
     pd.testing.assert_frame_equal(cn_s, ref["cn_s"])
     pd.testing.assert_frame_equal(cn_g1, ref["cn_g1"])
@@ -190,3 +205,26 @@ def test_cell_in_two_libraries_is_refused(complete):
         s = pd.concat([s, s.iloc[[len(s) - 1]]], ignore_index=True)
     with pytest.raises(ValueError, match="more than one"):
         prep.process_input_data(s, g)
+
+
+def test_block_path_keys_serve_every_consumer():
+    """The block path's RegularKeys give the consumers of the keys (consensus profiles, the
+    clone prior's first rows, the general pivot) what the general path's TableKeys give."""
+    s = _table(9, "s", seed=4, order="cells_unsorted", shared=True)
+    g = _table(8, "g", seed=5, n_libs=3, order="cells_unsorted", shared=True)
+    cn_s, cn_g1, inp = prep.process_input_data(s, g)
+    assert isinstance(inp.keys_g, prep.RegularKeys)
+    kg = prep.TableKeys(cn_g1, "cell_id", "chr", "start")
+    np.testing.assert_array_equal(inp.keys_g.cell_code, kg.cell_code)
+    np.testing.assert_array_equal(inp.keys_g.locus_code, kg.locus_code)
+    np.testing.assert_array_equal(inp.keys_g.cells, kg.cells)
+    np.testing.assert_array_equal(inp.keys_g.loci_start, kg.loci_start)
+    assert inp.keys_g.regular == kg.regular
+    for col in ("state", "copy"):
+        pd.testing.assert_frame_equal(prep.consensus_clone_profiles(cn_g1, col, keys=inp.keys_g),
+                                      prep.consensus_clone_profiles(cn_g1, col, keys=kg))
+    np.testing.assert_array_equal(prep.first_clone(cn_s, inp.cells_s, keys=inp.keys_s),
+                                  prep.first_clone(cn_s, inp.cells_s))
+    p1 = prep.pivot_cells_by_loci(cn_g1, "reads", "cell_id", "chr", "start", inp.keys_g)
+    p2 = prep.pivot_cells_by_loci(cn_g1, "reads", "cell_id", "chr", "start")
+    np.testing.assert_array_equal(p1.values, p2.values)

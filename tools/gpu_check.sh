@@ -5,7 +5,9 @@
 set -o pipefail
 TAG=${1:-run}; shift || true
 mkdir -p gpurun_out
+# PYTEST_K: an optional -k expression (e.g. to leave out a test under rework)
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider \
+  ${PYTEST_K:+-k "$PYTEST_K"} \
   > gpurun_out/${TAG}_tests.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/${TAG}_tests.log; exit 1; }
 tail -2 gpurun_out/${TAG}_tests.log
 if [ "$1" != "--quick" ]; then

@@ -730,12 +730,64 @@ def _group_median(group: np.ndarray, values: np.ndarray, n_groups: int) -> np.nd
     return out
 
 
+def _consensus_blocks(cn: pd.DataFrame, col_name: str, clone_col: str, cn_state_col, keys: "RegularKeys"):
+    """consensus_clone_profiles' medians on a regular sorted table (every cell one block of
+    the same L loci, one clone per cell): the (L, cells) matrix of ``col_name``, each cell's
+    modal state, each clone's majority ploidy (row counts are L per cell, so cell counts
+    decide), and per clone a column median over its kept cells.  (L, n_clones) and the
+    sorted clone ids, or None (NaN values or states, a cell in two clones: the general path)."""
+    B, L = keys.cells.size, keys.regular
+    clone = cn[clone_col].to_numpy()
+    if clone.size != B * L or not _constant_rows(clone, B, L):
+        return None
+    kcell, ku = _sorted_codes(clone[::L])
+    if "None" in set(ku.tolist()):                       # clone 'None' is removed (:63)
+        bad = int(np.flatnonzero(ku == "None")[0])
+        kcell = np.where(kcell == bad, -1, kcell)
+    vals = cn[col_name].to_numpy(np.float64).reshape(B, L)
+    if np.isnan(vals).any():
+        return None
+    keep = kcell >= 0
+    if cn_state_col is not None:
+        st = cn[cn_state_col].to_numpy().reshape(B, L)
+        if st.dtype.kind not in "iu":
+            if st.dtype.kind != "f" or np.isnan(st).any() or not (st == np.floor(st)).all():
+                return None
+        lo, hi = int(st.min()), int(st.max())
+        if lo < 0 or hi >= 4096:
+            return None
+        sti = st.astype(np.int64)
+        cnt = np.bincount((np.arange(B, dtype=np.int64)[:, None] * (hi + 1) + sti).reshape(-1),
+                          minlength=B * (hi + 1)).reshape(B, hi + 1)
+        pl = cnt.argmax(axis=1)                          # modal state, ties to the smallest
+        pu = np.unique(pl)
+        pc = np.searchsorted(pu, pl)
+        cc = np.bincount(kcell[keep] * len(pu) + pc[keep], minlength=len(ku) * len(pu)).reshape(len(ku), len(pu))
+        keep &= pc == cc.argmax(axis=1)[np.where(kcell >= 0, kcell, 0)]
+    med = np.full((L, len(ku)), np.nan)
+    for c in range(len(ku)):
+        rows = keep & (kcell == c)
+        if rows.any():
+            med[:, c] = np.median(vals[rows], axis=0)
+    return med, ku
+
+
 def consensus_clone_profiles(cn: pd.DataFrame, col_name: str, clone_col="clone_id", cell_col="cell_id",
                              chr_col="chr", start_col="start", cn_state_col="state", keys=None) -> pd.DataFrame:
     """compute_consensus_clone_profiles (:42-88): median of ``col_name`` per (locus, clone)
     over the clone's majority-ploidy cells; index (chr, start) sorted as pivot_table sorts
     it, columns the sorted clone ids.  Integer codes, row masks and one lexsort; the long
     table itself is never copied."""
+    if (isinstance(keys, RegularKeys) and _n_rows(keys) == len(cn)
+            and isinstance(cn[chr_col].dtype, pd.CategoricalDtype)):
+        fast = _consensus_blocks(cn, col_name, clone_col, cn_state_col, keys)
+        if fast is not None:
+            med, ku = fast
+            chr_lab = pd.Categorical(keys.loci_chr, categories=cn[chr_col].cat.categories,
+                                     ordered=cn[chr_col].cat.ordered)
+            idx = pd.MultiIndex.from_arrays([chr_lab, keys.loci_start], names=[chr_col, start_col])
+            prof = pd.DataFrame(med, index=idx, columns=pd.Index(ku, name=clone_col))
+            return prof.dropna(how="all").dropna(axis=1, how="all").sort_index()
     kc, ku = _sorted_codes(cn[clone_col].to_numpy())
     if "None" in set(ku.tolist()):                       # clone 'None' is removed (:63)
         bad = int(np.flatnonzero(ku == "None")[0])

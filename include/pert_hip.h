@@ -214,6 +214,36 @@ int pert_adam(const pert_problem* prob, pert_state* st, const pert_adam_hparams*
  * left bit-identical.  Steps 2/3 shards only. */
 int pert_stream_ceiling(const pert_problem* prob, pert_state* st, hipStream_t stream);
 
+/* tau initialiser (guess_times, pert_model.py:426-457): the k-means / EM stage of
+ * manhattan_binarization (:364-375 -- standardisation, GaussianMixture(n_components=2,
+ * random_state=0): k-means++ and Lloyd initialisation, then EM) for every cell in ONE launch,
+ * in fp64, twice per cell: run 0 breaks exact ties on a k-means decision towards centre 1,
+ * run 1 towards centre 0.  The levels / skew / threshold scan that follow stay on the host
+ * side of the ABI (tau_init.py).  Decisions that fp32 rounding (the reference's arithmetic)
+ * could flip are reported in flags so the caller recomputes those cells exactly. */
+typedef struct {
+  int32_t first;                   /* k-means++ first centre index (RandomState(0) draw) */
+  int32_t lloyd_max_iter;          /* 300 (KMeans default) */
+  int32_t em_max_iter;             /* 100 (GaussianMixture default) */
+  int32_t pad_;
+  double u[2];                     /* the two local-trial uniforms of k-means++ */
+  double tie;                      /* relative width of an exact tie on a k-means decision */
+  double pp_margin;                /* k-means++ draw / choice margin, relative to the potential */
+  double fragile;                  /* Lloyd shift-vs-tol margin, relative to tol */
+  double em_margin;                /* EM |lower-bound change| vs tol margin, absolute */
+  double em_tol;                   /* 1e-3 */
+  double reg_covar;                /* 1e-6 */
+} pert_tau_params;
+
+/* norm: float [N][L] CN-normalised reads, one contiguous row per cell (device).
+ * Outputs (device): labels int8 [2][N][L] final k-means labels per run (1 = centre 1);
+ * scratch int8 [2][N][L] workspace; means double [2][N][2] the GMM means per run;
+ * flags int32 [2][N] per run: bit 0 a Lloyd / EM stopping decision within its margin,
+ * bit 1 a k-means++ draw within its margin whose alternatives end in other labels. */
+int pert_tau_kmeans_em(int32_t L, int32_t N, const float* norm, const pert_tau_params* p,
+                       int8_t* labels, int8_t* scratch, double* means, int32_t* flags,
+                       hipStream_t stream);
+
 /* Test-only entry points: the per-(bin, cell) arithmetic of pert_math.h evaluated on
  * the host (no GPU needed) or on the device, for the parity suite.  Not used by any
  * product path. */

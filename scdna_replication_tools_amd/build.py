@@ -20,9 +20,10 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SOURCES = [os.path.join(HERE, "csrc", "pert_kernels.hip")]
+SOURCES = [os.path.join(HERE, "csrc", "pert_kernels.hip"), os.path.join(HERE, "csrc", "tau_kernels.hip")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", "pert_math.h"), os.path.join(ROOT, "include", "pert_hip.h")]
 OUT = os.path.join(HERE, "libpert_hip.so")
+OBJ_DIR = os.path.join(HERE, "build_obj")
 ARCH = os.environ.get("PERT_OFFLOAD_ARCH", "gfx950")
 HASH_LEN = 16
 FLAGS = ["-fno-slp-vectorize", "-fno-signed-zeros"]
@@ -60,23 +61,60 @@ def up_to_date() -> bool:
     return embedded_hash(OUT) == source_hash()
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
-        return OUT
-    # -fno-slp-vectorize: SLP packs independent fp32 chains into v_pk_* pairs whose register
-    # pairing and shuffles cost 50-70 VGPRs in the enumerated passes (occupancy), for no gain
-    cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-shared", "-fPIC", *FLAGS,
-           "-DPERT_SOURCE_HASH=\"{}\"".format(source_hash()),
-           "-I" + os.path.join(ROOT, "include"), *SOURCES, "-o", OUT + ".tmp"]
+def _object_hash(src: str) -> str:
+    """Hash of one translation unit's inputs: the source, the shared headers, arch and flags."""
+    h = hashlib.sha256()
+    for d in [src] + DEPS[len(SOURCES):]:
+        with open(d, "rb") as fh:
+            h.update(fh.read())
+    h.update(ARCH.encode())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()[:HASH_LEN]
+
+
+def _run(cmd, what, verbose=False):
     if verbose:
-        cmd.append("-Rpass-analysis=kernel-resource-usage")
         print(" ".join(cmd), flush=True)
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         sys.stderr.write(res.stdout + res.stderr)
-        raise RuntimeError("hipcc failed building {}".format(OUT))
+        raise RuntimeError("hipcc failed building {}".format(what))
     if verbose:
         sys.stderr.write(res.stderr)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Each source is compiled to its own object (kept beside OUT, named by the hash of its
+    inputs, so an unchanged source is not recompiled); pert_version() with the whole tree's
+    source_hash() is a one-line object of its own; then one link."""
+    if not force and up_to_date():
+        return OUT
+    # -fno-slp-vectorize: SLP packs independent fp32 chains into v_pk_* pairs whose register
+    # pairing and shuffles cost 50-70 VGPRs in the enumerated passes (occupancy), for no gain
+    base = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", *FLAGS, "-I" + os.path.join(ROOT, "include")]
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(OBJ_DIR, "{}.{}.o".format(os.path.splitext(os.path.basename(src))[0], _object_hash(src)))
+        if force or not os.path.exists(obj):
+            os.makedirs(OBJ_DIR, exist_ok=True)
+            cmd = base + ["-c", src, "-o", obj + ".tmp"]
+            if verbose:
+                cmd.append("-Rpass-analysis=kernel-resource-usage")
+            _run(cmd, obj, verbose)
+            os.replace(obj + ".tmp", obj)
+        objs.append(obj)
+    ver = os.path.join(OBJ_DIR, "pert_version.c")
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    with open(ver, "w") as fh:
+        # "src=<hash>": the sources this binary was compiled from (_native.lib() refuses a
+        # library whose hash differs from its tree)
+        fh.write('const char* pert_version(void) {{ return "pert_hip 0.2 {} src={}"; }}\n'.format(ARCH, source_hash()))
+    _run([os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-c", ver, "-o", ver[:-2] + ".o"], ver, verbose)
+    _run([hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs, ver[:-2] + ".o", "-o", OUT + ".tmp"], OUT,
+         verbose)
+    for f in os.listdir(OBJ_DIR):                       # objects of older sources
+        if f.endswith(".o") and os.path.join(OBJ_DIR, f) not in objs and f != "pert_version.o":
+            os.remove(os.path.join(OBJ_DIR, f))
     os.replace(OUT + ".tmp", OUT)
     return OUT
 

@@ -2081,12 +2081,9 @@ int selftest_enum_host(int64_t n, const float* x, const float* em1, const float*
 // ============================================================================ C ABI
 extern "C" {
 
-// "src=<hash>": SHA-256 prefix of the sources this binary was compiled from (build.py
-// source_hash(); _native.lib() refuses a library whose hash differs from its tree)
-#ifndef PERT_SOURCE_HASH
-#define PERT_SOURCE_HASH "unknown"
-#endif
-const char* pert_version(void) { return "pert_hip 0.2 gfx950 src=" PERT_SOURCE_HASH; }
+// pert_version() ("... src=<hash>", the SHA-256 prefix of every source of the library) is
+// compiled by build.py into a one-line object of its own, so a change to one source
+// recompiles only that source's object.
 
 int pert_make_layout(int32_t L, int32_t N, int32_t K1, int32_t n_libs, pert_layout* o) {
   if (!o || L <= 0 || N <= 0 || K1 < 1 || K1 > PERT_MAX_K1 || n_libs < 1) return PERT_E_ARG;

@@ -228,11 +228,22 @@ def binarization_fraction(Xraw: torch.Tensor, return_fragile: bool = False, retu
     disagreeing, a k-means++ candidate draw next to a cumulative-sum boundary), and
     ``near``: the partition is certain but the levels' fp32 rounding could move the scan
     (a flat minimum, points within the levels' rounding budget of the chosen threshold) --
-    and also returns the (L, N) k-means labels (True = centre 1)."""
+    and also returns the (L, N) k-means labels (True = centre 1).
+
+    On a GPU the k-means / EM stage of both runs is one launch of the HIP kernel
+    (pert_tau_kmeans_em, csrc/tau_kernels.hip); on the CPU it is the tensor program
+    ``_kmeans_em``.  The levels and the threshold scan are tensor programs either way."""
+    X, Xc = _standardize(Xraw)
     if not return_fragile:
-        return _binarize(Xraw, 0.0)[0]
-    f_hi, fr_hi, pp_hi, sc_hi, mn_hi, lab_hi = _binarize(Xraw, TIE, with_minor=True)
-    f_lo, fr_lo, pp_lo, sc_lo, mn_lo, lab_lo = _binarize(Xraw, -TIE, with_minor=True)
+        mu, fr, _, _ = _kmeans_em(X, Xc, 0.0)
+        return _levels_scan(X, Xc, mu, fr)[0]
+    if X.device.type == "cuda":
+        (mu_hi, fr_hi, pp_hi, lab_hi), (mu_lo, fr_lo, pp_lo, lab_lo) = kmeans_em_native(Xraw)
+    else:
+        mu_hi, fr_hi, pp_hi, lab_hi = _kmeans_em(X, Xc, TIE)
+        mu_lo, fr_lo, pp_lo, lab_lo = _kmeans_em(X, Xc, -TIE)
+    f_hi, fr_hi, sc_hi, mn_hi = _levels_scan(X, Xc, mu_hi, fr_hi)
+    f_lo, fr_lo, sc_lo, mn_lo = _levels_scan(X, Xc, mu_lo, fr_lo)
     labels = fr_hi | fr_lo | (f_hi != f_lo) | pp_hi | pp_lo | (lab_hi != lab_lo).any(0)
     near = sc_hi | sc_lo | (mn_hi > 0) | (mn_lo > 0)
     if return_minor:
@@ -240,16 +251,23 @@ def binarization_fraction(Xraw: torch.Tensor, return_fragile: bool = False, retu
     return f_hi, labels | near
 
 
-def _binarize(Xraw: torch.Tensor, tie_bias: float, with_minor: bool = False):
+def _standardize(Xraw: torch.Tensor):
+    """(X - mean) / std per column in fp64 (pert_model.py:367), and X centred again (KMeans
+    centres its data first)."""
     X = Xraw.to(torch.float64)
-    L, N = X.shape
     X = (X - X.mean(0)) / X.std(0, unbiased=False)
+    return X, X - X.mean(0)
+
+
+def _kmeans_em(X: torch.Tensor, Xc: torch.Tensor, tie_bias: float):
+    """The k-means / EM stage as one tensor program over the columns: k-means++ (with the
+    alternative second centres where a draw sits on a rounding boundary), Lloyd, EM.
+    Returns (GMM means (2, N), fragile (N,), k-means++ fragile (N,), labels (L, N) bool)."""
+    L, N = X.shape
     first, u = _rng_draws(L)
-    Xc = X - X.mean(0)                                               # KMeans centres the data first
     tol = Xc.var(0, unbiased=False) * 1e-4
     fragile = torch.zeros(N, dtype=torch.bool, device=X.device)
     frag_pp = torch.zeros(N, dtype=torch.bool, device=X.device)
-    frag_scan = torch.zeros(N, dtype=torch.bool, device=X.device)
     alts = []
     cen = _kmeans_pp(Xc, first, u, frag_pp, alts)
     lab1 = _lloyd(Xc, cen, tol, fragile=fragile, tie_bias=tie_bias)
@@ -265,6 +283,53 @@ def _binarize(Xraw: torch.Tensor, tie_bias: float, with_minor: bool = False):
             same &= (lab_a == lab1[:, idx]).all(0) & ~fr_a
         frag_pp[idx[same]] = False
     mu = _gmm_means(X, lab1, fragile=fragile)
+    return mu, fragile, frag_pp, lab1
+
+
+def tau_params(L: int):
+    """The pert_tau_params of the k-means / EM stage at L bins (the constants of this module
+    and the sklearn defaults the reference runs)."""
+    from ._native import PertTauParams
+    first, u = _rng_draws(L)
+    p = PertTauParams()
+    p.first, p.lloyd_max_iter, p.em_max_iter = first, 300, 100
+    p.u[0], p.u[1] = float(u[0]), float(u[1])
+    p.tie, p.pp_margin, p.fragile, p.em_margin = TIE, PP_MARGIN, FRAGILE, EM_MARGIN
+    p.em_tol, p.reg_covar = 1e-3, 1e-6
+    return p
+
+
+def kmeans_em_native(Xraw: torch.Tensor):
+    """``_kmeans_em`` of both tie directions in one launch of pert_tau_kmeans_em (HIP,
+    csrc/tau_kernels.hip) on Xraw's device and current stream: [(means (2, N), fragile,
+    k-means++ fragile, labels (L, N) bool) for tie +TIE, then -TIE]."""
+    import ctypes
+    from . import _native
+    L, N = Xraw.shape
+    dev = Xraw.device
+    norm = Xraw.to(torch.float32).T.contiguous()                     # (N, L): one row per cell
+    labels = torch.empty((2, N, L), dtype=torch.int8, device=dev)
+    scratch = torch.empty((2, N, L), dtype=torch.int8, device=dev)
+    means = torch.empty((2, N, 2), dtype=torch.float64, device=dev)
+    flags = torch.empty((2, N), dtype=torch.int32, device=dev)
+    p = tau_params(L)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _native.check(_native.lib().pert_tau_kmeans_em(L, N, norm.data_ptr(), ctypes.byref(p), labels.data_ptr(),
+                                                   scratch.data_ptr(), means.data_ptr(), flags.data_ptr(),
+                                                   ctypes.c_void_p(stream)), "pert_tau_kmeans_em")
+    out = []
+    for r in range(2):
+        out.append((means[r].T, (flags[r] & 1) != 0, (flags[r] & 2) != 0, labels[r].T.bool()))
+    return out
+
+
+def _levels_scan(X: torch.Tensor, Xc: torch.Tensor, mu: torch.Tensor, fragile: torch.Tensor):
+    """The levels (GMM means, or percentiles chosen by the skew when the means are close)
+    and the 100-threshold scan (pert_model.py:375-423) for every column, with the rounding
+    margins of the scan.  Returns (fraction, fragile, scan fragile, minor)."""
+    L, N = X.shape
+    fragile = fragile.clone()
+    frag_scan = torch.zeros(N, dtype=torch.bool, device=X.device)
     gap = (mu[0] - mu[1]).abs()
     b0, b1 = torch.minimum(mu[0], mu[1]), torch.maximum(mu[0], mu[1])
     close = gap < MEAN_GAP_THRESH
@@ -327,9 +392,7 @@ def _binarize(Xraw: torch.Tensor, tie_bias: float, with_minor: bool = False):
         frag_scan[s:s + chunk] |= (((dcnt > 0) | (near > 0)) & (d - dmin <= slack)).any(0)
         minor[s:s + chunk] = near_best[0]
     frac = (X > best[None, :]).sum(0).to(torch.float64) / L
-    if with_minor:
-        return frac, fragile, frag_pp, frag_scan, minor, lab1
-    return frac, fragile | frag_pp | frag_scan | (minor > 0)
+    return frac, fragile, frag_scan, minor
 
 
 # ------------------------------------------------------------------------------------------

@@ -38,6 +38,7 @@ exact path against sklearn and the whole against prep.guess_times, up to 5,451 b
 from __future__ import annotations
 
 import os
+import threading
 import time
 
 import numpy as np
@@ -46,6 +47,15 @@ import torch
 # imports them): the exact host path calls them
 from scipy.stats import skew
 from sklearn.cluster._kmeans import _kmeans_single_lloyd, _tolerance
+
+# sklearn wraps its Lloyd in a threadpoolctl limit of 1 BLAS thread (utils/parallel.py
+# _threadpool_controller_decorator), which sets and restores OpenBLAS's thread count around
+# every call.  From the exact path's threads those calls race each other and the BLAS calls
+# of the other threads (openblas_set_num_threads during a BLAS call in flight), which
+# deadlocked a 10k-cell run; the unwrapped function is called instead.  Its BLAS work (gemm of
+# a 256-sample chunk by 2 one-feature centres) is below OpenBLAS's threading threshold, so it
+# runs on one thread either way and the labels are the same.
+_lloyd_unwrapped = getattr(_kmeans_single_lloyd, "__wrapped__", _kmeans_single_lloyd)
 
 MEAN_GAP_THRESH = 0.7
 EARLY_S_SKEW_THRESH = 0.2
@@ -454,7 +464,7 @@ def exact_kmeans_labels(x: np.ndarray) -> np.ndarray:
     dc = _sq_dist_upcast(X[cand], X)
     np.minimum(closest, dc, out=dc)
     centers[1] = X[cand[np.argmin(dc @ sw.reshape(-1, 1))]]
-    labels, _, _, _ = _kmeans_single_lloyd(X, sw, centers, max_iter=300, verbose=False, tol=tol, n_threads=1)
+    labels, _, _, _ = _lloyd_unwrapped(X, sw, centers, max_iter=300, verbose=False, tol=tol, n_threads=1)
     return labels.astype(np.int8)
 
 
@@ -486,11 +496,15 @@ class _HostHelper:
     ``np.dot``).  ``get()`` is None when either is not available; the numpy restatement then
     runs the same operations (same results, slower)."""
     _inst = False
+    _lock = threading.Lock()
 
     @classmethod
     def get(cls):
-        if cls._inst is False:
-            cls._inst = cls._load()
+        # loaded once, under a lock: threadpoolctl's library scan (dl_iterate_phdr) from
+        # several of the exact path's threads at once is not safe
+        with cls._lock:
+            if cls._inst is False:
+                cls._inst = cls._load()
         return cls._inst
 
     @staticmethod
@@ -707,6 +721,7 @@ def exact_fractions(norm_cols: np.ndarray, labels=None, n_threads: int = 1, chun
     chunks of cells on ``n_threads`` threads (numpy releases the GIL in the array work)."""
     Xs_all = standardize_rows(np.asarray(norm_cols, dtype=F32).T)
     n = Xs_all.shape[0]
+    _HostHelper.get()                       # before the threads start
     out = np.empty(n, np.float64)
 
     def run(lo, hi):

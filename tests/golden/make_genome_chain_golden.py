@@ -7,7 +7,7 @@ from the per-cell sklearn restatement of guess_times.  tests/test_gpu_chain.py r
 ``scRT(...).infer(level='pyro')`` on the same tables and compares loss traces, stopping
 iterations, decodes and final sites with this fixture.
 
-    python tests/golden/make_genome_chain_golden.py [--chunked]   (about 45 minutes on 8 CPU threads)
+    python tests/golden/make_genome_chain_golden.py [--chunked | --fp64]   (35-90 minutes on 8 CPU threads)
 """
 import os
 import sys
@@ -27,21 +27,25 @@ OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "genome_chain_ora
 # the same algebra whose only difference is the summation order -- how far two correct fp32
 # runs drift apart over a genome-length fit (the envelope the product is held to)
 OUT_CHUNKED = os.path.join(os.path.dirname(os.path.abspath(__file__)), "genome_chain_oracle_chunked.npz")
+# the same chain in fp64: how far the fp32 reference's own trajectory sits from exact arithmetic
+# (the product evaluates some terms more accurately than fp32 autograd)
+OUT_F64 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "genome_chain_oracle_f64.npz")
 
 
 def main():
     chunked = "--chunked" in sys.argv
+    f64 = "--fp64" in sys.argv
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     s, g, truth = genome_tables()
     digest = input_digest(s, g)
     m = genome_scrt(s, g, device="cpu")._pert_model()
     t0 = time.perf_counter()
-    res = oracle_chain(m, torch.float32, log=lambda msg: print(msg, "{:.1f}s".format(time.perf_counter() - t0),
+    res = oracle_chain(m, torch.float64 if f64 else torch.float32, log=lambda msg: print(msg, "{:.1f}s".format(time.perf_counter() - t0),
                                                                flush=True), cell_chunk=16 if chunked else None)
     res["input_digest"] = np.array(digest)
     res["cells_s"] = np.asarray(m._prepare().cells_s).astype("U")
     res["cells_g"] = np.asarray(m._prepare().cells_g).astype("U")
-    out = OUT_CHUNKED if chunked else OUT
+    out = OUT_F64 if f64 else (OUT_CHUNKED if chunked else OUT)
     np.savez_compressed(out, **res)
     print("wrote", out, os.path.getsize(out), "bytes; losses", len(res["losses_g"]), len(res["losses_s"]),
           len(res["losses_s2"]))

@@ -45,6 +45,15 @@ def main():
     t_sim = time.perf_counter() - t0
     print("simulated {} + {} cells x {} bins in {:.1f} s".format(n, n, sim.n_bins, t_sim), file=sys.stderr, flush=True)
     torch.zeros(1, device="cuda")
+    # a heartbeat on stderr while the fit runs (a GPU command silent for minutes is taken as hung)
+    import threading
+    t_fit = time.perf_counter()
+    beat = threading.Event()
+
+    def heartbeat():
+        while not beat.wait(20.0):
+            print("... fit running {:.0f} s".format(time.perf_counter() - t_fit), file=sys.stderr, flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
     import contextlib
     fit_stdout = contextlib.redirect_stdout(sys.stderr)          # the fit's own prints (convergence lines)
     fit_stdout.__enter__()
@@ -67,6 +76,7 @@ def main():
                             n_jobs=args.n_jobs)
         cn_s_out, supp_s, cn_g1_out, supp_g1 = m.run_pert_model()
         clusters_ok = None
+    beat.set()
     print("fit done: {}".format(m.timings), file=sys.stderr, flush=True)
     fit_stdout.__exit__(None, None, None)
     acc_cn = float((cn_s_out["model_cn_state"] == cn_s_out["true_somatic_cn"]).mean())

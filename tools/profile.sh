@@ -10,7 +10,7 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 ARGS=${*:-"--steps 10 --warmup 2 --no-cpu-baseline"}
 cd /tmp && export TMPDIR=/tmp
-K='--kernel-include-regex enum_|enum3_|obs_kernel|finalize_kernel|adam_kernel'
+K='--kernel-include-regex enum_|enum3_|obs_|finalize_kernel|adam_kernel'
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 "$R/bench.py" $ARGS > "$OUT/trace.log" 2>&1
 i=0
 for PMC in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_LDS" \

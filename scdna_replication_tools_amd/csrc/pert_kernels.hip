@@ -989,31 +989,30 @@ __global__ void __launch_bounds__(64) obs_pair_kernel(pert_problem pr, pert_stat
   const float c0 = (1.0f - lam) / lam;
   const float log1m_lam = logf(1.0f - lam);
 
-  float ucc[2], tau[2], beta[2][K1T];
+  // the pair's parameters as packed (rep-0 copy, rep-1 copy) values
+  pf2 ucc = {0.0f, 0.0f}, tau = {0.5f, 0.5f}, beta[K1T];
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    ucc[r] = 0.0f;
-    tau[r] = 0.5f;
+  for (int k = 0; k < K1T; ++k) beta[k] = pf2{0.0f, 0.0f};
+  if (valid) {
 #pragma unroll
-    for (int k = 0; k < K1T; ++k) beta[r][k] = 0.0f;
-    if (valid) {
+    for (int r = 0; r < 2; ++r) {
       const int n = g + r * NG;
-      ucc[r] = st.params[lay.off_u + n] * c0;
-#pragma unroll
-      for (int k = 0; k < K1T; ++k)
-        if (k < K1) beta[r][k] = st.params[lay.off_beta + k * N + n];
+      const float uc = st.params[lay.off_u + n] * c0;
       float dm;
-      tau[r] = clipped_sigmoid(st.params[lay.off_tau + n], &dm);
+      const float tr = clipped_sigmoid(st.params[lay.off_tau + n], &dm);
+      if (r == 0) { ucc.x = uc; tau.x = tr; } else { ucc.y = uc; tau.y = tr; }
+#pragma unroll
+      for (int k = 0; k < K1T; ++k) {
+        const float b = (k < K1) ? st.params[lay.off_beta + k * N + n] : 0.0f;
+        if (r == 0) beta[k].x = b; else beta[k].y = b;
+      }
     }
   }
-  float acc[2][K1T], accT[2];
+  pf2 acc[K1T], accT = {0.0f, 0.0f};
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    accT[r] = 0.0f;
-#pragma unroll
-    for (int k = 0; k < K1T; ++k) acc[r][k] = 0.0f;
-  }
-  float loss = 0.0f, ga = 0.0f, dsum = 0.0f, gdd = 0.0f;
+  for (int k = 0; k < K1T; ++k) acc[k] = pf2{0.0f, 0.0f};
+  pf2 loss2 = {0.0f, 0.0f}, ga2 = {0.0f, 0.0f}, dsum2 = {0.0f, 0.0f}, gdd2 = {0.0f, 0.0f};
+  const float vmask = valid ? 1.0f : 0.0f;
   __syncthreads();                                   // s_bc written by the wave's lanes
 
   // register software pipeline: the reads and CN of the next kObsU bins are in flight while
@@ -1038,44 +1037,63 @@ __global__ void __launch_bounds__(64) obs_pair_kernel(pert_problem pr, pert_stat
 #pragma unroll
     for (int u = 0; u < kObsU; ++u) { xg[u] = xq[u]; cg[u] = (float)cq[u]; }
     if (lg + kObsU < l1) load_group(lg + kObsU);
+    float gts[kObsU];
 #pragma unroll
     for (int u = 0; u < kObsU; ++u) {
+      gts[u] = 0.0f;
       const int l = lg + u;
-      if (l >= l1) break;
+      if (l >= l1) continue;
       const float x = xg[u], cnf = cg[u];
       const float* bcl = s_bc + (l - l0) * (K1T + 1);
       const float rho = bcl[0];
+      pf2 dot = {0.0f, 0.0f};
       float gf[K1T];
 #pragma unroll
-      for (int k = 0; k < K1T; ++k) gf[k] = (k < K1) ? bcl[1 + k] : 0.0f;
-      const float invx = x > 0.0f ? frcp(x) : 0.0f;
-      float gt_sum = 0.0f;
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        float dot = 0.0f;
-#pragma unroll
-        for (int k = 0; k < K1T; ++k) dot += beta[r][k] * gf[k];
-        const float omega = fexp(dot);
-        const float t = tau[r] - rho;
-        const float phi = 1.0f / (1.0f + fexp(-a_val * t));
-        ObsOut o;
-        obs_cellbin(x, invx, cnf, (float)r, log1m_lam, ucc[r] * omega, phi, o);
-        if (valid) {
-          loss += o.ll;
-          gt_sum += o.gt;
-          accT[r] += a_val * o.gt;
-          ga += t * o.gt;
-          dsum += o.dsum;
-          gdd += o.gdd;
-          const float ge = o.gD * omega;
-#pragma unroll
-          for (int k = 0; k < K1T; ++k) acc[r][k] += ge * gf[k];
-        }
+      for (int k = 0; k < K1T; ++k) {
+        gf[k] = (k < K1) ? bcl[1 + k] : 0.0f;
+        dot += beta[k] * gf[k];
       }
-      const float ws = wave_sum(gt_sum);
-      if (lane == 0) s_bin[l - l0] = ws;
+      const float invx = x > 0.0f ? frcp(x) : 0.0f;
+      const pf2 omega = {fexp(dot.x), fexp(dot.y)};
+      const pf2 t = tau - rho;
+      const pf2 at = t * (-a_val);
+      const pf2 phi = {frcp(1.0f + fexp(at.x)), frcp(1.0f + fexp(at.y))};
+      ObsPairOut o;
+      obs_pair_cellbin(x, invx, cnf, log1m_lam, ucc * omega, phi, o);
+      const pf2 gt = o.gt * vmask;
+      loss2 += o.ll * vmask;
+      accT += gt * a_val;
+      ga2 += t * gt;
+      dsum2 += o.dsum * vmask;
+      gdd2 += o.gdd * vmask;
+      const pf2 ge = o.gD * omega * vmask;
+#pragma unroll
+      for (int k = 0; k < K1T; ++k) acc[k] += ge * gf[k];
+      gts[u] = gt.x + gt.y;
+    }
+    // the per-bin rho sums of the kObsU bins over the wave's 64 lanes: a butterfly that halves
+    // the values per lane at each exchange (2 + 1 + 4 shuffles for 4 bins, not 4 x 6)
+    static_assert(kObsU == 4, "butterfly written for 4 bins");
+    const bool hi32 = (lane & 32) != 0, hi16 = (lane & 16) != 0;
+    float a0 = hi32 ? gts[2] : gts[0], a1 = hi32 ? gts[3] : gts[1];      // keep
+    float b0 = hi32 ? gts[0] : gts[2], b1 = hi32 ? gts[1] : gts[3];      // send
+    a0 += __shfl_xor(b0, 32, 64);
+    a1 += __shfl_xor(b1, 32, 64);
+    float c = hi16 ? a1 : a0;
+    c += __shfl_xor(hi16 ? a0 : a1, 16, 64);
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    // lane (hi32, hi16) holds bin lg + 2 hi32 + hi16
+    if ((lane & 15) == 0) {
+      const int lb = lg + (hi32 ? 2 : 0) + (hi16 ? 1 : 0);
+      if (lb < l1) s_bin[lb - l0] = c;
     }
   }
+  float acc_out[2][K1T];
+#pragma unroll
+  for (int k = 0; k < K1T; ++k) { acc_out[0][k] = acc[k].x; acc_out[1][k] = acc[k].y; }
+  const float accT_out[2] = {accT.x, accT.y};
+  const float loss = loss2.x + loss2.y, ga = ga2.x + ga2.y, dsum = dsum2.x + dsum2.y, gdd = gdd2.x + gdd2.y;
   __syncthreads();
   for (int i = lane; i < l1 - l0; i += 64) st.bin_part[(size_t)blockIdx.x * pr.L + l0 + i] = s_bin[i];
   if (valid) {
@@ -1085,8 +1103,8 @@ __global__ void __launch_bounds__(64) obs_pair_kernel(pert_problem pr, pert_stat
       const int n = g + r * NG;
 #pragma unroll
       for (int k = 0; k < K1T; ++k)
-        if (k < K1) cp[(size_t)k * N + n] = acc[r][k];
-      cp[(size_t)K1 * N + n] = accT[r];
+        if (k < K1) cp[(size_t)k * N + n] = acc_out[r][k];
+      cp[(size_t)K1 * N + n] = accT_out[r];
     }
   }
   const double bl = wave_sum_d((double)loss);

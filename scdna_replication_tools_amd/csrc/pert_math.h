@@ -685,6 +685,68 @@ PERT_HD void obs_cellbin(float x, float invx, float cn, float rep, float log1m_l
   }
 }
 
+// Step 1 in pair mode (pert_hip.h): the two copies of one G1/2 cell.bin -- rep 0 and rep 1,
+// chi = (cn, 2 cn), each copy with its own D = u omega (1-lam)/lam and phi -- together in packed
+// fp32 (v_pk_fma / mul / add_f32: both copies per VALU issue; transcendentals stay per element).
+// The same terms as obs_cellbin for each copy.  Where both copies have delta >= kAsymMin (every
+// copy with cn > 0 at 500 kb coverage) the asymptotic series runs packed; any other pair takes
+// obs_cellbin per copy (clamped / shifted delta).
+struct ObsPairOut {
+  pf2 ll, gD, dsum, gdd, gt;
+};
+
+PERT_HD void obs_pair_cellbin(float x, float invx, float cn, float log1m_lam, pf2 D, pf2 phi, ObsPairOut& o) {
+  const pf2 chi = {cn, 2.0f * cn};
+  const pf2 d = chi * D;
+  pf2 ll, gD, dsum, gdd, gt;
+  if (d.x >= kAsymMin && d.y >= kAsymMin) {
+    // Bernoulli(phi) of rep 0 / rep 1 with the clamps of pert_model.py:622-623
+    const pf2 phic = {fmed3(phi.x, 0.001f, 0.999f), fmed3(phi.y, 0.001f, 0.999f)};
+    const pf2 lb = pf2{__builtin_amdgcn_logf_or_log2(1.0f - phic.x), __builtin_amdgcn_logf_or_log2(phic.y)} * kLn2;
+    gt = pf2{phic.x == phi.x ? -phic.x : 0.0f, phic.y == phi.y ? 1.0f - phic.y : 0.0f};
+    const pf2 r = {frcp(d.x), frcp(d.y)};
+    const pf2 zs = d + x;
+    const pf2 rz = {frcp(zs.x), frcp(zs.y)};
+    const pf2 q = r * x;                                // x/d
+    const pf2 iu = d * rz;                              // 1/(1 + x/d)
+    const pf2 u = q + 1.0f;
+    const pf2 lu = pf2{__builtin_amdgcn_logf_or_log2(u.x), __builtin_amdgcn_logf_or_log2(u.y)} * kLn2;
+    const pf2 l1 = lu + (q - (u - 1.0f)) * iu;          // log1p(x/d), log1p_corr
+    // log1p(d/x), direct (the hoisted log1p(x/d) + log(d/x) cancels where x >> d); 0 when x == 0
+    const pf2 q2 = d * invx;
+    const pf2 u2 = q2 + 1.0f;
+    const pf2 lu2 = pf2{__builtin_amdgcn_logf_or_log2(u2.x), __builtin_amdgcn_logf_or_log2(u2.y)} * kLn2;
+    const pf2 l2 = lu2 + (q2 - (u2 - 1.0f)) * (rz * x);
+    const pf2 r2 = r * r, rz2 = rz * rz;
+    const pf2 sr = r * (0.0833333333333333333f - r2 * (0.00277777777777777778f - r2 * 0.000793650793650793651f));
+    const pf2 srz = rz * (0.0833333333333333333f - rz2 * (0.00277777777777777778f - rz2 * 0.000793650793650793651f));
+    const pf2 lam = (d - 0.5f) * l1 + x * l2 + (srz - sr);
+    const pf2 r4 = r2 * r2, rz4 = rz2 * rz2;
+    const pf2 psi = l1 - 0.5f * (rz - r) - 0.0833333333333333333f * (rz2 - r2)
+                    + 0.00833333333333333333f * (rz4 - r4) - 0.00396825396825396825f * (rz4 * rz2 - r4 * r2);
+    const pf2 g = psi + log1m_lam;
+    ll = lb + (d * log1m_lam + lam);
+    gD = chi * g;
+    gdd = d * g;
+    dsum = d;
+  } else {
+    ObsOut a;
+    obs_cellbin(x, invx, cn, 0.0f, log1m_lam, D.x, phi.x, a);
+    const float ll0 = a.ll, gD0 = a.gD, ds0 = a.dsum, gdd0 = a.gdd, gt0 = a.gt;
+    obs_cellbin(x, invx, cn, 1.0f, log1m_lam, D.y, phi.y, a);
+    ll = pf2{ll0, a.ll};
+    gD = pf2{gD0, a.gD};
+    dsum = pf2{ds0, a.dsum};
+    gdd = pf2{gdd0, a.gdd};
+    gt = pf2{gt0, a.gt};
+  }
+  o.ll = ll;
+  o.gD = gD;
+  o.dsum = dsum;
+  o.gdd = gdd;
+  o.gt = gt;
+}
+
 // ----------------------------------------------------------------- transforms
 // _clipped_sigmoid (torch/distributions/transforms.py:629-631); *mask = 0 where clipped.
 PERT_HD float clipped_sigmoid(float zz, float* dmask) {

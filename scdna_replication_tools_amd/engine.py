@@ -598,14 +598,16 @@ class PertShard:
             nat.check(self.lib.pert_adam(ctypes.byref(self._prob), ctypes.byref(self._state),
                                          ctypes.byref(self._hp), self._stream()), "pert_adam")
 
-    def run_svi(self, max_iter: int, min_iter: int, rel_tol: float, chunk: int = 8, depth: int = 2):
+    def run_svi(self, max_iter: int, min_iter: int, rel_tol: float, chunk: int = 8, depth: int = 8):
         """The SVI loop of pert_model.py:742-758 (:800-816, :867-883) without a per-step host
         synchronisation.  Every iteration's loss is recorded on the device and the reference's
         stopping rule (rel-tol plateau after min_iter, NaN) is evaluated there
         (include/pert_hip.h, loop_ctl); launches of iterations after the stopping one are
         no-ops.  The host queues iterations ahead, copies the loss records back every
         ``chunk`` iterations and stops queueing once a copied record shows the stop (it is
-        at most ``chunk * depth`` iterations ahead).  Returns (losses, reason) with
+        at most ``chunk * depth`` iterations ahead: 64 by default, tens of ms of queued work
+        even for a 0.5 ms step, so a fit thread that waits for the GIL behind the helper
+        thread's host work does not leave the device idle).  Returns (losses, reason) with
         reason 0 = max_iter reached, 1 = converged, 2 = NaN loss; the fit state is the one
         after the last recorded iteration, exactly as if the loop had run on the host."""
         n = int(max_iter)

@@ -448,6 +448,12 @@ class pert_infer_scRT():
                 chr_col=self.chr_col, start_col=self.start_col, cn_state_col=self.cn_state_col, keys=keys_g)
             return prof, time.perf_counter() - t0
 
+        phases = self.timings.setdefault("phases", [])      # (phase, end time since the call began)
+        phases.clear()
+
+        def mark(name):
+            phases.append((name, round(time.perf_counter() - t_all, 4)))
+
         try:
             fut_prof = []
             tic = time.perf_counter()
@@ -480,13 +486,16 @@ class pert_infer_scRT():
             lb_g2 = np.concatenate([inp.libs_g, inp.libs_g])
             init1 = init_params(KIND_STEP1, None, lb_g2, n_libs, P, K, seed=self.seed, method=self.init_method,
                                 mean_reads=np.concatenate([mean_g, mean_g]), n_bins=inp.reads_g.shape[0])
+            mark("prep")
             s1 = self._shard_pairs(dd, inp.reads_g, inp.states_g, lb_g2, init1)
+            mark("init_shard1")
             logging.info('STEP 1: Learning reads to CN bias from low variance cells.')
             losses_g = self._svi(s1, self.max_iter_step1, self.min_iter_step1, "step1")
             c1 = s1.constrained()
             lambda_fit = np.asarray(c1["expose_lambda"], dtype=np.float32)
             beta_means_fit = np.asarray(c1["expose_beta_means"], dtype=np.float32)
             del s1
+            mark("step1")
 
             # ---- step 2: S cells, enumerated (:776-830)
             tic = time.perf_counter()
@@ -495,6 +504,7 @@ class pert_infer_scRT():
             # wall time step 1 did not hide (the helper's own durations: timings["helper_*"])
             self.timings["guess_times_s"] = time.perf_counter() - tic
             self.timings["helper_priors"], self.timings["helper_guess_times_s"] = t_priors, t_guess
+            mark("wait_priors")
             # (the helper runs its tasks in order: the two tau initialisers never share the pool)
             fut_prep3 = helper.submit(on_device, self._prep_step3, inp, profiles) if self.run_step3 else None
             ploidy = etas.argmax_states().astype(np.float32).mean(0)
@@ -502,8 +512,10 @@ class pert_infer_scRT():
                                 beta_means=beta_means_fit, seed=self.seed, method=self.init_method)
             s2 = self._shard(KIND_STEP2, dd, inp.reads_s, inp.libs_s, init2, eta=etas, lamb=float(lambda_fit[0]),
                              beta_means=beta_means_fit)
+            mark("init_shard2")
             logging.info('STEP 2: Jointly infer replication and CN states in high variance cells.')
             losses_s = self._svi(s2, self.max_iter, self.min_iter, "step2")
+            mark("step2")
             tic = time.perf_counter()
             cn_map, rep_map, c2 = self._decode(s2, dd)
             trace_s = MapTrace(cn=cn_map, rep=rep_map, expose_u=c2["expose_u"], expose_rho=c2["expose_rho"],
@@ -514,6 +526,7 @@ class pert_infer_scRT():
             rho_fit = c2["expose_rho"]
             a_fit = c2["expose_a"]
             del s2
+            mark("decode_package2")
 
             cn_g1_out = supp_g1_out_df = None
             if self.run_step3:
@@ -528,8 +541,10 @@ class pert_infer_scRT():
                 s3 = self._shard(KIND_STEP3, dd, inp.reads_g, inp.libs_g, init3, eta=etas2, lamb=float(lambda_fit[0]),
                                  beta_means=beta_means_fit, rho_fixed=np.asarray(rho_fit).reshape(-1),
                                  a_fixed=float(np.asarray(a_fit)[0]))
+                mark("init_shard3")
                 logging.info('STEP 3: Running pre-trained S-phase model on low variance cells.')
                 losses_s2 = self._svi(s3, self.max_iter_step3, self.min_iter_step3, "step3")
+                mark("step3")
                 tic = time.perf_counter()
                 cn3, rep3, c3 = self._decode(s3, dd)
                 trace_s2 = MapTrace(cn=cn3, rep=rep3, expose_u=c3["expose_u"], expose_rho=rho_fit, expose_a=a_fit,
@@ -538,6 +553,7 @@ class pert_infer_scRT():
                     self.cn_g1, trace_s2, self._axes(inp.cells_g, inp.keys_g), lambda_fit, losses_g, losses_s2)
                 self.timings["decode_package_g"] = time.perf_counter() - tic
                 del s3
+                mark("decode_package3")
         finally:
             # also when a fit or a helper task raised: no helper work outlives the call
             helper.shutdown(wait=True, cancel_futures=True)

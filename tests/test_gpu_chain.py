@@ -135,6 +135,8 @@ def test_genome_length_chain_matches_oracle_fixture():
     np.testing.assert_array_equal(scrt.model.t_init_s, fx["t_init_s"])
     np.testing.assert_array_equal(scrt.model.t_init_g, fx["t_init_g"])
     prod = product_arrays(scrt.model, *out)
+    if os.environ.get("PERT_DUMP_DIR"):                     # for offline analysis of a lease run
+        np.savez_compressed(os.path.join(os.environ["PERT_DUMP_DIR"], "genome_chain_product.npz"), **prod)
     rep = _compare(prod, fx)
     from tests import _bounds
     _bounds.write_report("genome_chain_64x64x5451", {k: (list(v) if isinstance(v, tuple) else v) for k, v in rep.items()})

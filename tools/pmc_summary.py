@@ -18,7 +18,8 @@ from collections import defaultdict
 
 
 def short(name):
-    for k in ("enum_kernel", "enum_dma_kernel", "enum3_kernel", "obs_kernel", "finalize_kernel", "scalar_kernel",
+    for k in ("enum_kernel", "enum_dma_kernel", "enum3_kernel", "obs_kernel", "obs_pair_kernel", "finalize_kernel",
+              "scalar_kernel", "tau_kmeans_em_kernel",
               "adam_kernel"):
         if k in name:
             return name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]

@@ -112,6 +112,29 @@ def test_tutorial_cell9_verbatim_matches_chained_oracle_fixture():
 
 
 GENOME = os.path.join(os.path.dirname(__file__), "golden", "genome_chain_oracle.npz")
+# the same oracle chain with another fp32 summation order, and in fp64 (make_genome_chain_golden.py
+# --chunked / --fp64): how far two correct evaluations of the reference's algebra drift apart
+# over a genome-length fit -- the envelope the product is held to where the fp32 trajectory
+# itself is not reproducible
+GENOME_ALTS = {"chunked": os.path.join(os.path.dirname(__file__), "golden", "genome_chain_oracle_chunked.npz"),
+               "fp64": os.path.join(os.path.dirname(__file__), "golden", "genome_chain_oracle_f64.npz")}
+STEP1_WINDOW = 300        # step-1 iterations before the oracle variants themselves drift apart (~307)
+
+
+def _scaled_dev(a, b, n=None):
+    """max |a - b| over the common length (or the first n) relative to the trace's scale max |b|
+    (the ELBO crosses zero during the fits, so a per-value relative error is meaningless there)."""
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    m = min(len(a), len(b)) if n is None else min(n, len(a), len(b))
+    return float(np.abs(a[:m] - b[:m]).max() / np.abs(b).max())
+
+
+def _sites(x, ref):
+    return {"lam": float(abs(x["lam"].ravel()[0] - ref["lam"].ravel()[0]) / ref["lam"].ravel()[0]),
+            "a": float(abs(x["a"].ravel()[0] - ref["a"].ravel()[0]) / ref["a"].ravel()[0]),
+            "rho": float(np.abs(x["rho"].ravel() - ref["rho"].ravel()).max()),
+            "tau_s": float(np.abs(x["tau_s"] - ref["tau_s"]).max()),
+            "u_s": float((np.abs(x["u_s"] - ref["u_s"]) / np.abs(ref["u_s"])).max())}
 
 
 def test_genome_length_chain_matches_oracle_fixture():
@@ -119,13 +142,27 @@ def test_genome_length_chain_matches_oracle_fixture():
     two libraries) through the reference's entry point with its defaults
     (``scRT(...).infer(level='pyro')``: max_iter 2000 / min_iter 100 / rel_tol 1e-6, steps
     1 and 3 at half) against the committed fp32 oracle chain
-    (tests/golden/make_genome_chain_golden.py): the same t_init for every cell (the exact
-    tau initialiser), the same stopping iteration of every fit, loss traces within 1e-4,
-    decodes >= 99.9 %, final sites close."""
+    (tests/golden/make_genome_chain_golden.py):
+
+    * the same t_init for every cell (the exact tau initialiser);
+    * loss traces within 1e-4 of the trace's scale: steps 2 and 3 whole, step 1 over its first
+      300 iterations -- step 1 ends in an undamped oscillation (1,000 iterations, no
+      convergence) in which two fp32 evaluations of the same algebra drift 4.7 % apart after
+      ~307 iterations, so its whole trace is held to twice the oracle variants' spread;
+    * the stopping iteration of every fit inside the range the oracle variants stop in (fp32,
+      fp32 in another summation order, fp64: step 2 stops at 1,151 / 1,151 / 1,187), +- 2 %;
+    * decodes >= 99.9 % equal on the S cells, and on the G1/2 cells fitted in the same tau mode;
+      a G1/2 cell's step-3 posterior is bimodal (tau ~ 0, or tau ~ 1 with u about halved: a G1
+      profile fits as fully replicated) and a cell started mid-way (t_init ~ 0.47) takes either
+      mode by trajectory details (tools/genome_mode_probe.py: the product alone, with another
+      tile length -- another order of the same per-cell sums -- flips a second cell;
+      profiles/r03i_mode_probe.log) -- at most 2 of the 64 such cells may take the other mode;
+    * final lambda, a, rho, tau, u within twice the oracle variants' spread."""
     from tests._configs import genome_scrt, genome_tables, input_digest
-    if not os.path.exists(GENOME):
-        pytest.skip("tests/golden/genome_chain_oracle.npz not generated (tests/golden/make_genome_chain_golden.py)")
+    if not os.path.exists(GENOME) or not all(os.path.exists(f) for f in GENOME_ALTS.values()):
+        pytest.skip("genome oracle fixtures not generated (tests/golden/make_genome_chain_golden.py)")
     fx = dict(np.load(GENOME))
+    alts = {k: dict(np.load(f)) for k, f in GENOME_ALTS.items()}
     s, g, truth = genome_tables()
     assert input_digest(s, g) == str(fx["input_digest"]), "genome inputs changed"
     scrt = genome_scrt(s, g)
@@ -137,8 +174,42 @@ def test_genome_length_chain_matches_oracle_fixture():
     prod = product_arrays(scrt.model, *out)
     if os.environ.get("PERT_DUMP_DIR"):                     # for offline analysis of a lease run
         np.savez_compressed(os.path.join(os.environ["PERT_DUMP_DIR"], "genome_chain_product.npz"), **prod)
-    rep = _compare(prod, fx)
+
+    rep = {"traces": {}, "stops": {}, "sites": {}, "sites_envelope": {}}
+    for key in ("losses_g", "losses_s", "losses_s2"):
+        env = max(_scaled_dev(a[key], fx[key]) for a in alts.values())
+        r = {"dev": _scaled_dev(prod[key], fx[key]), "envelope": env}
+        if key == "losses_g":
+            r["dev_first_%d" % STEP1_WINDOW] = _scaled_dev(prod[key], fx[key], STEP1_WINDOW)
+        rep["traces"][key] = r
+        stops = [len(fx[key])] + [len(a[key]) for a in alts.values()]
+        rep["stops"][key] = {"product": len(prod[key]), "oracles": stops}
+    env_sites = {k: max(_sites(a, fx)[k] for a in alts.values()) for k in ("lam", "a", "rho", "tau_s", "u_s")}
+    rep["sites"], rep["sites_envelope"] = _sites(prod, fx), env_sites
+    agree_s = float(((prod["cn_s"] == fx["cn_s"]) & (prod["rep_s"] == fx["rep_s"])).mean())
+    same_mode = np.abs(prod["tau_g"] - fx["tau_g"]) < 0.5
+    flipped = [int(i) for i in np.flatnonzero(~same_mode)]
+    agree_g = float(((prod["cn_g"] == fx["cn_g"]) & (prod["rep_g"] == fx["rep_g"]))[:, same_mode].mean())
+    rep.update(cn_s_agree=agree_s, cn_g_agree_same_mode=agree_g, g1_mode_flips=flipped,
+               g1_mode_flips_t_init=[float(fx["t_init_g"][i]) for i in flipped],
+               cn_g_agree_all=float(((prod["cn_g"] == fx["cn_g"]) & (prod["rep_g"] == fx["rep_g"])).mean()))
     from tests import _bounds
-    _bounds.write_report("genome_chain_64x64x5451", {k: (list(v) if isinstance(v, tuple) else v) for k, v in rep.items()})
+    _bounds.write_report("genome_chain_64x64x5451", rep)
+    print("genome chain vs oracle:", rep)
+
+    for key, r in rep["traces"].items():
+        if key == "losses_g":
+            assert r["dev_first_%d" % STEP1_WINDOW] <= 1e-4, (key, r)
+            assert r["dev"] <= 2 * r["envelope"], (key, r)
+        else:
+            assert r["dev"] <= 1e-4, (key, r)
+    for key, r in rep["stops"].items():
+        lo, hi = min(r["oracles"]), max(r["oracles"])
+        assert lo - 0.02 * lo <= r["product"] <= hi + 0.02 * hi, (key, r)
+    for k, v in rep["sites"].items():
+        assert v <= 2 * env_sites[k] + 1e-6, (k, v, env_sites[k])
+    assert agree_s >= 0.999, agree_s
+    assert agree_g >= 0.999, agree_g
+    assert len(flipped) <= 2 and all(0.3 <= t <= 0.7 for t in rep["g1_mode_flips_t_init"]), rep
     m = out[0].merge(truth, on=['cell_id', 'chr', 'start'])
     assert (m['model_cn_state'] == m['true_somatic_cn']).mean() > 0.99

@@ -3,7 +3,9 @@ every gradient element inside the Appendix C bound (tests/_bounds.py) against th
 oracle.
 
 * configs[2] / configs[3] (C3 / C4): the full 5,451-bin 500 kb genome at the configs'
-  coverage (1e6 reads per cell), a 64-cell shard, clone and composite priors, steps 1-3;
+  coverage (1e6 reads per cell), a 64-cell shard, clone and composite priors -- including the
+  reference's default g1_composite prior exactly as the product builds it (prep + code book,
+  tests/_problems.py prior="product_composite") -- steps 1-3;
 * configs[4] (C5): an 8-cell shard of the 136,275-bin 20 kb grid (about 7 reads per bin,
   the small-delta NB branch);
 * C4 at full size (10,000 cells x 5,451 bins) through the product's pass: the per-cell
@@ -53,7 +55,7 @@ def _parity(case, kind, prob, kw, z):
         assert r["rel_l2"] <= GRAD_RTOL, (name, r["rel_l2"])
 
 
-@pytest.mark.parametrize("prior", ["clone", "composite"])
+@pytest.mark.parametrize("prior", ["clone", "composite", "product_composite"])
 def test_c3_c4_full_genome_shard_step2(prior):
     prob, kw, z = make_problem("step2", L=5451, N=64, prior=prior, num_reads=1e6, seed=21)
     _parity("c3c4_shard_step2_" + prior, "step2", prob, kw, z)

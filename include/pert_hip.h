@@ -214,18 +214,20 @@ int pert_adam(const pert_problem* prob, pert_state* st, const pert_adam_hparams*
  * left bit-identical.  Steps 2/3 shards only. */
 int pert_stream_ceiling(const pert_problem* prob, pert_state* st, hipStream_t stream);
 
-/* tau initialiser (guess_times, pert_model.py:426-457): the k-means / EM stage of
- * manhattan_binarization (:364-375 -- standardisation, GaussianMixture(n_components=2,
- * random_state=0): k-means++ and Lloyd initialisation, then EM) for every cell in ONE launch,
- * in fp64, twice per cell: run 0 breaks exact ties on a k-means decision towards centre 1,
- * run 1 towards centre 0.  The levels / skew / threshold scan that follow stay on the host
- * side of the ABI (tau_init.py).  Decisions that fp32 rounding (the reference's arithmetic)
- * could flip are reported in flags so the caller recomputes those cells exactly. */
+/* tau initialiser (guess_times, pert_model.py:426-457): the batched pass of
+ * manhattan_binarization (:364-423) for every cell in ONE launch, in fp64 -- standardisation,
+ * GaussianMixture(n_components=2, random_state=0) (k-means++ and Lloyd initialisation, then EM),
+ * the levels (GMM means, or percentiles chosen by the skew), the 100-threshold Manhattan scan --
+ * twice per cell: run 0 breaks exact ties on a k-means decision towards centre 1, run 1 towards
+ * centre 0.  Decisions that fp32 rounding (the reference's arithmetic) could flip are reported
+ * in flags, so the caller recomputes those cells exactly (tau_init.exact_fractions). */
 typedef struct {
   int32_t first;                   /* k-means++ first centre index (RandomState(0) draw) */
   int32_t lloyd_max_iter;          /* 300 (KMeans default) */
   int32_t em_max_iter;             /* 100 (GaussianMixture default) */
+  int32_t q_lo[5], q_hi[5];        /* np.percentile 'linear' at q = .05 .25 .5 .75 .95: floor(q (L-1)), +1 (<= L-1) */
   int32_t pad_;
+  double q_t[5];                   /* q (L-1) - floor(q (L-1)) */
   double u[2];                     /* the two local-trial uniforms of k-means++ */
   double tie;                      /* relative width of an exact tie on a k-means decision */
   double pp_margin;                /* k-means++ draw / choice margin, relative to the potential */
@@ -233,16 +235,27 @@ typedef struct {
   double em_margin;                /* EM |lower-bound change| vs tol margin, absolute */
   double em_tol;                   /* 1e-3 */
   double reg_covar;                /* 1e-6 */
+  double mean_gap;                 /* 0.7  (MEAN_GAP_THRESH) */
+  double early_skew, late_skew;    /* 0.2, -0.2 */
+  double fragile_abs;              /* margin of the mean-gap / skew thresholds, absolute */
+  double level_margin;             /* relative rounding budget of the scan levels (1e-6 sqrt(L)) */
+  double eps32;                    /* float32 eps: the reference's summation noise in the scan */
 } pert_tau_params;
 
 /* norm: float [N][L] CN-normalised reads, one contiguous row per cell (device).
- * Outputs (device): labels int8 [2][N][L] final k-means labels per run (1 = centre 1);
- * scratch int8 [2][N][L] workspace; means double [2][N][2] the GMM means per run;
- * flags int32 [2][N] per run: bit 0 a Lloyd / EM stopping decision within its margin,
- * bit 1 a k-means++ draw within its margin whose alternatives end in other labels. */
-int pert_tau_kmeans_em(int32_t L, int32_t N, const float* norm, const pert_tau_params* p,
-                       int8_t* labels, int8_t* scratch, double* means, int32_t* flags,
-                       hipStream_t stream);
+ * Outputs (device), per run r (0: ties to centre 1, 1: ties to centre 0) and cell n:
+ *   labels  int8 [2][N][L]  final k-means labels (1 = centre 1)
+ *   scratch int8 [2][N][L]  workspace
+ *   means   double [2][N][2] GMM means
+ *   flags   int32 [2][N]    bit 0: a Lloyd / EM stopping decision or the mean-gap / skew test
+ *                           within its margin; bit 1: a k-means++ draw within its margin whose
+ *                           alternatives end in other labels; bit 2: the scan's minimum within
+ *                           its rounding slack of another threshold's
+ *   frac    double [2][N]   replicated fraction (the reference's t_init where no flag is set)
+ *   minor   double [2][N]   points within the levels' rounding budget of the chosen threshold */
+int pert_tau_binarize(int32_t L, int32_t N, const float* norm, const pert_tau_params* p,
+                      int8_t* labels, int8_t* scratch, double* means, int32_t* flags, double* frac,
+                      double* minor, hipStream_t stream);
 
 /* Test-only entry points: the per-(bin, cell) arithmetic of pert_math.h evaluated on
  * the host (no GPU needed) or on the device, for the parity suite.  Not used by any

@@ -27,7 +27,7 @@ BLOCK = 256
 EXPORTED_SYMBOLS = (
     "pert_make_layout", "pert_workspace_sizes", "pert_auto_bins_per_tile", "pert_enum_pass", "pert_obs_pass",
     "pert_finalize", "pert_adam", "pert_enum_step", "pert_adam_shared", "pert_stream_ceiling", "pert_selftest_nb_lgdiff_host",
-    "pert_selftest_nb_lgdiff_device", "pert_selftest_enum_cellbin_host", "pert_tau_kmeans_em", "pert_version",
+    "pert_selftest_nb_lgdiff_device", "pert_selftest_enum_cellbin_host", "pert_tau_binarize", "pert_version",
 )
 
 
@@ -68,9 +68,12 @@ class PertState(ctypes.Structure):
 
 
 class PertTauParams(ctypes.Structure):
-    _fields_ = [("first", c_int32), ("lloyd_max_iter", c_int32), ("em_max_iter", c_int32), ("pad_", c_int32),
+    _fields_ = [("first", c_int32), ("lloyd_max_iter", c_int32), ("em_max_iter", c_int32),
+                ("q_lo", c_int32 * 5), ("q_hi", c_int32 * 5), ("pad_", c_int32), ("q_t", c_double * 5),
                 ("u", c_double * 2), ("tie", c_double), ("pp_margin", c_double), ("fragile", c_double),
-                ("em_margin", c_double), ("em_tol", c_double), ("reg_covar", c_double)]
+                ("em_margin", c_double), ("em_tol", c_double), ("reg_covar", c_double), ("mean_gap", c_double),
+                ("early_skew", c_double), ("late_skew", c_double), ("fragile_abs", c_double),
+                ("level_margin", c_double), ("eps32", c_double)]
 
 
 class PertAdamHparams(ctypes.Structure):
@@ -149,8 +152,8 @@ def load(path: str):
     handle.pert_selftest_nb_lgdiff_device.argtypes = [i64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     handle.pert_selftest_enum_cellbin_host.argtypes = [i32, i64, fp, fp, fp, fp, c_float, fp, fp, fp, fp,
                                                        fp, fp, fp, POINTER(i32)]
-    handle.pert_tau_kmeans_em.argtypes = [i32, i32, c_void_p, POINTER(PertTauParams), c_void_p, c_void_p, c_void_p,
-                                          c_void_p, c_void_p]
+    handle.pert_tau_binarize.argtypes = [i32, i32, c_void_p, POINTER(PertTauParams), c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_void_p]
     handle.pert_version.restype = c_char_p
     for name in EXPORTED_SYMBOLS:
         if name != "pert_version":

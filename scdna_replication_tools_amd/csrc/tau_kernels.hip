@@ -152,14 +152,97 @@ __device__ __forceinline__ double chunk_scan(double v, double carry, double* tot
   return pre + v;
 }
 
-__global__ __launch_bounds__(kT) void tau_kmeans_em_kernel(int L, int N, const float* __restrict__ norm,
+// Order-preserving map of a double onto uint64 (radix select) and back.
+__device__ __forceinline__ uint64_t okey(double v) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double ikey(uint64_t k) {
+  return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k));
+}
+
+// Order statistics rank[0..3] (0-based) of the standardised profile by 8-bit radix select,
+// MSB first (8 passes, one 256-bin integer histogram per target in LDS: deterministic).
+__device__ void select4(const Cell& c, const int (&rank)[4], double (&out)[4], uint32_t* hist, uint64_t* s_pref,
+                        long long* s_k) {
+  const int L = c.L;
+  if (threadIdx.x < 4) {
+    s_pref[threadIdx.x] = 0;
+    s_k[threadIdx.x] = rank[threadIdx.x];
+  }
+  for (int pass = 0; pass < 8; ++pass) {
+    const int shift = 56 - 8 * pass;
+    for (int i = threadIdx.x; i < 4 * 256; i += kT) hist[i] = 0;
+    __syncthreads();
+    uint64_t pref[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pref[j] = s_pref[j];
+    for (int i = threadIdx.x; i < L; i += kT) {
+      const uint64_t key = okey(c.X(i));
+      const uint32_t dig = (uint32_t)(key >> shift) & 255u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (pass == 0 || (key >> (shift + 8)) == (pref[j] >> (shift + 8))) atomicAdd(&hist[j * 256 + dig], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+      const int j = threadIdx.x;
+      long long cum = 0;
+      for (int d = 0; d < 256; ++d) {
+        const long long h = hist[j * 256 + d];
+        if (cum + h > s_k[j]) {
+          s_pref[j] = pref[j] | ((uint64_t)d << shift);
+          s_k[j] -= cum;
+          break;
+        }
+        cum += h;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) out[j] = ikey(s_pref[j]);
+}
+
+// first index i in [0, 100) with th[i] >= v (th ascending), i.e. #{i : th[i] < v}
+__device__ __forceinline__ int count_below(const double* th, double v) {
+  int lo = 0, hi = 100;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (th[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+// #{i : th[i] <= v}
+__device__ __forceinline__ int count_le(const double* th, double v) {
+  int lo = 0, hi = 100;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (th[mid] <= v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+constexpr double kFix = 4294967296.0;     // 2^32: fixed-point scale of the scan's LDS histograms
+
+__global__ __launch_bounds__(kT) void tau_binarize_kernel(int L, int N, const float* __restrict__ norm,
                                                              pert_tau_params p, int8_t* __restrict__ labels,
                                                              int8_t* __restrict__ scratch,
                                                              double* __restrict__ means,
-                                                             int32_t* __restrict__ flags) {
+                                                             int32_t* __restrict__ flags,
+                                                             double* __restrict__ frac_out,
+                                                             double* __restrict__ minor_out) {
   __shared__ double sm[8 * kTW];
   __shared__ double sval[4];
   __shared__ int smi[kTW];
+  __shared__ uint32_t s_hist[4 * 256];
+  __shared__ uint64_t s_pref[4];
+  __shared__ long long s_k[4];
+  __shared__ double s_th[100];
+  __shared__ unsigned long long s_h0[101], s_h1[101];
+  __shared__ int s_hn[101], s_e[101];
+  __shared__ double s_d[100];
+  __shared__ int s_cnt[100], s_near[100];
   const int n = blockIdx.x, run = blockIdx.y;
   if (n >= N) return;
   const double tie = run == 0 ? p.tie : -p.tie;
@@ -369,23 +452,134 @@ __global__ __launch_bounds__(kT) void tau_kmeans_em_kernel(int L, int N, const f
     if (fabs(fabs(change) - p.em_tol) <= p.em_margin) fragile = true;
     if (fabs(change) < p.em_tol) break;
   }
+  // ---- levels (pert_model.py:377-400; tau_init._levels_scan): the GMM means, or percentiles of
+  // the profile chosen by its skew when the means are closer than MEAN_GAP_THRESH
+  double b0 = fmin(mu0, mu1), b1 = fmax(mu0, mu1);
+  const double gap = fabs(mu0 - mu1);
+  if (fabs(gap - p.mean_gap) <= p.fragile_abs) fragile = true;
+  if (gap < p.mean_gap) {
+    double m[2] = {0.0, 0.0};
+    for (int i = threadIdx.x; i < L; i += kT) {
+      const double xc = c.Xc(i);
+      m[0] += xc * xc;
+      m[1] += xc * xc * xc;
+    }
+    block_sums<2>(m, sm);
+    const double m2 = m[0] / (double)L, m3 = m[1] / (double)L;
+    const double sk = m3 / pow(m2, 1.5);
+    if (fabs(sk - p.early_skew) <= p.fragile_abs || fabs(sk - p.late_skew) <= p.fragile_abs) fragile = true;
+    const bool early = sk > p.early_skew, late = !early && sk < p.late_skew;
+    const int qa = early ? 2 : (late ? 0 : 1), qb = early ? 4 : (late ? 2 : 3);   // (50, 95) / (5, 50) / (25, 75)
+    const int rank[4] = {p.q_lo[qa], p.q_hi[qa], p.q_lo[qb], p.q_hi[qb]};
+    double v[4];
+    select4(c, rank, v, s_hist, s_pref, s_k);
+    // np.percentile 'linear' with numpy's two-sided lerp (tau_init._percentiles)
+    const double ta = p.q_t[qa], tb = p.q_t[qb];
+    const double da = v[1] - v[0], dbq = v[3] - v[2];
+    b0 = ta >= 0.5 ? v[1] - da * (1.0 - ta) : v[0] + da * ta;
+    b1 = tb >= 0.5 ? v[3] - dbq * (1.0 - tb) : v[2] + dbq * tb;
+  }
+
+  // ---- the 100-threshold scan (:402-423) with the rounding margins of tau_init._levels_scan.
+  // Threshold i binarises x to b1 iff x > th[i]; with c(x) = #{i : th[i] < x} the distance
+  // d(th[i]) = sum_{c(x) <= i} |x - b0| + sum_{c(x) > i} |x - b1| is a prefix sum over a
+  // 101-bin histogram of c(x) (fixed-point integer atomics: order-independent), and so are the
+  // counts above each threshold and the points within the margin window of each threshold.
+  for (int i = threadIdx.x; i < 101; i += kT) {
+    s_h0[i] = 0;
+    s_h1[i] = 0;
+    s_hn[i] = 0;
+    s_e[i] = 0;
+  }
+  if (threadIdx.x < 100) s_th[threadIdx.x] = threadIdx.x == 99 ? b1 : b0 + threadIdx.x * ((b1 - b0) / 99.0);
+  __syncthreads();
+  const double dbm = p.level_margin * fmax(fabs(b0), fabs(b1));
+  const double win = 2.0 * dbm + 1e-6;
+  double tmax = 0.0;
+  for (int i = threadIdx.x; i < L; i += kT) {
+    const double x = c.X(i);
+    const double e0 = fabs(x - b0), e1 = fabs(x - b1);
+    tmax = fmax(tmax, fmax(e0, e1));
+    const int cx = count_below(s_th, x);
+    atomicAdd(&s_h0[cx], (unsigned long long)(long long)llrint(e0 * kFix));
+    atomicAdd(&s_h1[cx], (unsigned long long)(long long)llrint(e1 * kFix));
+    atomicAdd(&s_hn[cx], 1);
+    const int lo = count_below(s_th, x - win), hi = count_le(s_th, x + win);   // |x - th[i]| <= win
+    if (lo < hi) {
+      atomicAdd(&s_e[lo], 1);
+      if (hi < 100) atomicAdd(&s_e[hi], -1);
+    }
+  }
+  {
+    double tm[1] = {tmax};
+    // block max through the sum helper's LDS: wave max, then the 4 waves
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) tm[0] = fmax(tm[0], __shfl_xor(tm[0], off, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = tm[0];
+    __syncthreads();
+    tmax = fmax(fmax(sm[0], sm[1]), fmax(sm[2], sm[3]));
+  }
+  if (threadIdx.x == 0) {
+    long long h0 = 0, h1t = 0, h1 = 0;
+    int hn = 0, hnt = 0, e = 0;
+    for (int k = 0; k < 101; ++k) {
+      h1t += (long long)s_h1[k];
+      hnt += s_hn[k];
+    }
+    for (int i = 0; i < 100; ++i) {
+      h0 += (long long)s_h0[i];
+      h1 += (long long)s_h1[i];
+      hn += s_hn[i];
+      e += s_e[i];
+      s_d[i] = (double)(h0 + (h1t - h1)) / kFix;
+      s_cnt[i] = hnt - hn;
+      s_near[i] = e;
+    }
+    int bi = 0;
+    for (int i = 1; i < 100; ++i)
+      if (s_d[i] < s_d[bi]) bi = i;                                   // first minimum
+    smi[0] = bi;
+  }
+  __syncthreads();
+  const int bi = smi[0];
+  const double dmin = s_d[bi];
+  const double near_best = (double)s_near[bi];
+  bool scan = false;
+  if (threadIdx.x < 100) {
+    const int i = threadIdx.x;
+    const double dcnt = fabs((double)(s_cnt[i] - s_cnt[bi]));
+    const double nr = (double)s_near[i];
+    const double noise = p.eps32 * (dcnt * 56.0 * 16.0 * tmax + (log2(dcnt + 1.0) + 2.0) * dmin);
+    const double mid = b0 + b1;
+    const double flip = fabs(mid - 2.0 * s_th[i]) + 4.0 * dbm;
+    const double flip_b = fabs(mid - 2.0 * s_th[bi]) + 4.0 * dbm;
+    const double slack = 2.0 * dcnt * dbm + nr * flip + near_best * flip_b + noise;
+    scan = (dcnt > 0.0 || nr > 0.0) && (s_d[i] - dmin <= slack);
+  }
+  const int any_scan = block_min_i(scan ? 0 : 1, smi) == 0;
+
   if (threadIdx.x == 0) {
     const size_t o = (size_t)run * N + n;
     means[2 * o] = mu0;
     means[2 * o + 1] = mu1;
-    flags[o] = (fragile ? 1 : 0) | (frag_pp ? 2 : 0);
+    flags[o] = (fragile ? 1 : 0) | (frag_pp ? 2 : 0) | (any_scan ? 4 : 0);
+    frac_out[o] = (double)s_cnt[bi] / (double)L;
+    minor_out[o] = near_best;
   }
 }
 
 }  // namespace
 
-extern "C" int pert_tau_kmeans_em(int32_t L, int32_t N, const float* norm, const pert_tau_params* p,
-                                  int8_t* labels, int8_t* scratch, double* means, int32_t* flags,
-                                  hipStream_t stream) {
-  if (L < 2 || N < 1 || !norm || !p || !labels || !scratch || !means || !flags) return PERT_E_ARG;
+extern "C" int pert_tau_binarize(int32_t L, int32_t N, const float* norm, const pert_tau_params* p,
+                                 int8_t* labels, int8_t* scratch, double* means, int32_t* flags, double* frac,
+                                 double* minor, hipStream_t stream) {
+  if (L < 2 || N < 1 || !norm || !p || !labels || !scratch || !means || !flags || !frac || !minor) return PERT_E_ARG;
   if (p->first < 0 || p->first >= L || p->lloyd_max_iter < 1 || p->em_max_iter < 1) return PERT_E_ARG;
-  hipLaunchKernelGGL(tau_kmeans_em_kernel, dim3(N, 2), dim3(kT), 0, stream, L, N, norm, *p, labels, scratch,
-                     means, flags);
+  for (int j = 0; j < 5; ++j)
+    if (p->q_lo[j] < 0 || p->q_lo[j] >= L || p->q_hi[j] < 0 || p->q_hi[j] >= L) return PERT_E_ARG;
+  hipLaunchKernelGGL(tau_binarize_kernel, dim3(N, 2), dim3(kT), 0, stream, L, N, norm, *p, labels, scratch,
+                     means, flags, frac, minor);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? PERT_OK : PERT_E_HIP_BASE + (int)e;
 }

@@ -240,20 +240,22 @@ def binarization_fraction(Xraw: torch.Tensor, return_fragile: bool = False, retu
     (a flat minimum, points within the levels' rounding budget of the chosen threshold) --
     and also returns the (L, N) k-means labels (True = centre 1).
 
-    On a GPU the k-means / EM stage of both runs is one launch of the HIP kernel
-    (pert_tau_kmeans_em, csrc/tau_kernels.hip); on the CPU it is the tensor program
-    ``_kmeans_em``.  The levels and the threshold scan are tensor programs either way."""
-    X, Xc = _standardize(Xraw)
-    if not return_fragile:
-        mu, fr, _, _ = _kmeans_em(X, Xc, 0.0)
-        return _levels_scan(X, Xc, mu, fr)[0]
-    if X.device.type == "cuda":
-        (mu_hi, fr_hi, pp_hi, lab_hi), (mu_lo, fr_lo, pp_lo, lab_lo) = kmeans_em_native(Xraw)
+    On a GPU the whole pass of both runs is one launch of the HIP kernel (pert_tau_binarize,
+    csrc/tau_kernels.hip); on the CPU it is the tensor programs ``_kmeans_em`` and
+    ``_levels_scan`` (the same algorithm, the same margins)."""
+    if return_fragile and Xraw.device.type == "cuda":
+        hi, lo = binarize_native(Xraw)
+        f_hi, fr_hi, pp_hi, sc_hi, mn_hi, lab_hi = hi["frac"], hi["fragile"], hi["pp"], hi["scan"], hi["minor"], hi["labels"]
+        f_lo, fr_lo, pp_lo, sc_lo, mn_lo, lab_lo = lo["frac"], lo["fragile"], lo["pp"], lo["scan"], lo["minor"], lo["labels"]
     else:
+        X, Xc = _standardize(Xraw)
+        if not return_fragile:
+            mu, fr, _, _ = _kmeans_em(X, Xc, 0.0)
+            return _levels_scan(X, Xc, mu, fr)[0]
         mu_hi, fr_hi, pp_hi, lab_hi = _kmeans_em(X, Xc, TIE)
         mu_lo, fr_lo, pp_lo, lab_lo = _kmeans_em(X, Xc, -TIE)
-    f_hi, fr_hi, sc_hi, mn_hi = _levels_scan(X, Xc, mu_hi, fr_hi)
-    f_lo, fr_lo, sc_lo, mn_lo = _levels_scan(X, Xc, mu_lo, fr_lo)
+        f_hi, fr_hi, sc_hi, mn_hi = _levels_scan(X, Xc, mu_hi, fr_hi)
+        f_lo, fr_lo, sc_lo, mn_lo = _levels_scan(X, Xc, mu_lo, fr_lo)
     labels = fr_hi | fr_lo | (f_hi != f_lo) | pp_hi | pp_lo | (lab_hi != lab_lo).any(0)
     near = sc_hi | sc_lo | (mn_hi > 0) | (mn_lo > 0)
     if return_minor:
@@ -296,23 +298,35 @@ def _kmeans_em(X: torch.Tensor, Xc: torch.Tensor, tie_bias: float):
     return mu, fragile, frag_pp, lab1
 
 
+QS = (0.05, 0.25, 0.5, 0.75, 0.95)          # the percentiles the levels may take (pert_model.py:388-399)
+
+
 def tau_params(L: int):
-    """The pert_tau_params of the k-means / EM stage at L bins (the constants of this module
-    and the sklearn defaults the reference runs)."""
+    """The pert_tau_params of the batched pass at L bins (the constants of this module and the
+    sklearn / numpy defaults the reference runs)."""
     from ._native import PertTauParams
     first, u = _rng_draws(L)
     p = PertTauParams()
     p.first, p.lloyd_max_iter, p.em_max_iter = first, 300, 100
+    for j, q in enumerate(QS):                       # as _percentiles computes them
+        pos = q * (L - 1)
+        lo = int(np.floor(pos))
+        p.q_lo[j], p.q_hi[j], p.q_t[j] = lo, min(lo + 1, L - 1), pos - lo
     p.u[0], p.u[1] = float(u[0]), float(u[1])
     p.tie, p.pp_margin, p.fragile, p.em_margin = TIE, PP_MARGIN, FRAGILE, EM_MARGIN
     p.em_tol, p.reg_covar = 1e-3, 1e-6
+    p.mean_gap, p.early_skew, p.late_skew = MEAN_GAP_THRESH, EARLY_S_SKEW_THRESH, LATE_S_SKEW_THRESH
+    p.fragile_abs, p.level_margin, p.eps32 = FRAGILE, _level_margin(L), EPS32
     return p
 
 
-def kmeans_em_native(Xraw: torch.Tensor):
-    """``_kmeans_em`` of both tie directions in one launch of pert_tau_kmeans_em (HIP,
-    csrc/tau_kernels.hip) on Xraw's device and current stream: [(means (2, N), fragile,
-    k-means++ fragile, labels (L, N) bool) for tie +TIE, then -TIE]."""
+def binarize_native(Xraw: torch.Tensor):
+    """The whole batched pass of both tie directions in ONE launch of pert_tau_binarize (HIP,
+    csrc/tau_kernels.hip) on Xraw's device and current stream: per run (tie +TIE, then -TIE)
+    a dict of the GMM means (2, N), the k-means labels (L, N) bool, the flags (fragile:
+    Lloyd / EM / mean-gap / skew margins; pp: a k-means++ draw; scan: the threshold scan's
+    slack), the replicated fraction and the scan's near-threshold count -- what ``_kmeans_em``
+    followed by ``_levels_scan`` compute as tensor programs."""
     import ctypes
     from . import _native
     L, N = Xraw.shape
@@ -322,15 +336,16 @@ def kmeans_em_native(Xraw: torch.Tensor):
     scratch = torch.empty((2, N, L), dtype=torch.int8, device=dev)
     means = torch.empty((2, N, 2), dtype=torch.float64, device=dev)
     flags = torch.empty((2, N), dtype=torch.int32, device=dev)
+    frac = torch.empty((2, N), dtype=torch.float64, device=dev)
+    minor = torch.empty((2, N), dtype=torch.float64, device=dev)
     p = tau_params(L)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    _native.check(_native.lib().pert_tau_kmeans_em(L, N, norm.data_ptr(), ctypes.byref(p), labels.data_ptr(),
-                                                   scratch.data_ptr(), means.data_ptr(), flags.data_ptr(),
-                                                   ctypes.c_void_p(stream)), "pert_tau_kmeans_em")
-    out = []
-    for r in range(2):
-        out.append((means[r].T, (flags[r] & 1) != 0, (flags[r] & 2) != 0, labels[r].T.bool()))
-    return out
+    _native.check(_native.lib().pert_tau_binarize(L, N, norm.data_ptr(), ctypes.byref(p), labels.data_ptr(),
+                                                  scratch.data_ptr(), means.data_ptr(), flags.data_ptr(),
+                                                  frac.data_ptr(), minor.data_ptr(), ctypes.c_void_p(stream)),
+                  "pert_tau_binarize")
+    return [dict(mu=means[r].T, labels=labels[r].T.bool(), fragile=(flags[r] & 1) != 0, pp=(flags[r] & 2) != 0,
+                 scan=(flags[r] & 4) != 0, frac=frac[r], minor=minor[r]) for r in range(2)]
 
 
 def _levels_scan(X: torch.Tensor, Xc: torch.Tensor, mu: torch.Tensor, fragile: torch.Tensor):

@@ -27,16 +27,11 @@ def main():
     torch.cuda.synchronize()
     for rep in range(2):
         t0 = time.perf_counter()
-        res = tau_init.kmeans_em_native(norm)
+        res = tau_init.binarize_native(norm)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        flags = [(int(r[1].sum()), int(r[2].sum())) for r in res]
-        print("kernel {:.4f} s, (fragile, kmeans++ fragile) per run {}".format(t1 - t0, flags), flush=True)
-    X, Xc = tau_init._standardize(norm)
-    t0 = time.perf_counter()
-    out = tau_init._levels_scan(X, Xc, res[0][0], res[0][1])
-    torch.cuda.synchronize()
-    print("levels/scan {:.4f} s".format(time.perf_counter() - t0), flush=True)
+        flags = [(int(r["fragile"].sum()), int(r["pp"].sum()), int(r["scan"].sum())) for r in res]
+        print("one-launch pass {:.4f} s, (fragile, kmeans++, scan) per run {}".format(t1 - t0, flags), flush=True)
     t0 = time.perf_counter()
     frac, lab_unsure, near, lab = tau_init.binarization_fraction(norm, return_fragile=True, return_minor=True)
     torch.cuda.synchronize()

@@ -21,7 +21,7 @@ from __future__ import annotations
 import ctypes
 import contextlib
 import math
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Callable, Dict, Optional
 
 import numpy as np
@@ -64,6 +64,10 @@ class EtaCodebook:
     """
     codes: np.ndarray   # (L, N) uint16
     table: np.ndarray   # (n_codes, P) float32 eta rows
+    # per-cell mean of the argmax states (pert_model.py:591-593), filled by the first
+    # argmax_states() / ploidy() call: the fit needs it for the init, the shard and the
+    # tau initialiser, and building the (L, N) states costs ~0.5 s at 10k cells
+    _ploidy: Optional[np.ndarray] = field(default=None, init=False, repr=False, compare=False)
 
     @property
     def P(self):
@@ -97,7 +101,7 @@ class EtaCodebook:
     def counts(self) -> np.ndarray:
         return np.bincount(self.codes.reshape(-1), minlength=self.table.shape[0])
 
-    def dirichlet_normaliser(self, mode: str = "torch32") -> float:
+    def dirichlet_normaliser(self, mode: str = "torch32", counts=None) -> float:
         """sum_{l,n} lgamma(sum eta) - sum lgamma(eta).  ``torch32`` evaluates each row in
         fp32 exactly as torch.distributions.Dirichlet.log_prob does on the CPU
         (dirichlet.py:93-97) -- the constant the reference adds to every loss --
@@ -106,26 +110,57 @@ class EtaCodebook:
         if mode == "exact":
             t = t.double()
         per = (torch.lgamma(t.sum(-1)) - torch.lgamma(t).sum(-1)).double().numpy()
-        return float((per * self.counts()).sum())
+        return float((per * (self.counts() if counts is None else np.asarray(counts))).sum())
 
     def argmax_states(self) -> np.ndarray:
         """torch.argmax(etas, dim=2) (first max), pert_model.py:591-592 and :439."""
         row_arg = np.argmax(self.table, axis=1)
-        return row_arg[self.codes]
+        states = row_arg[self.codes]
+        if self._ploidy is None:
+            self._ploidy = self._mean_states(states)
+        return states
+
+    @staticmethod
+    def _mean_states(states) -> np.ndarray:
+        # torch.mean(argmax.type(float32), dim=0) as the reference evaluates it (fp32, CPU)
+        return torch.mean(torch.as_tensor(states, dtype=torch.float32), dim=0).numpy()
+
+    def ploidy(self) -> np.ndarray:
+        """(N,) float32 mean argmax state per cell (pert_model.py:591-593), cached."""
+        if self._ploidy is None:
+            self.argmax_states()
+        return self._ploidy
+
+    def cells(self, sl: slice) -> "EtaCodebook":
+        """The code book of a contiguous range of cells (a rank's shard), ploidy cache included."""
+        sub = EtaCodebook(np.ascontiguousarray(self.codes[:, sl]), self.table)
+        if self._ploidy is not None:
+            sub._ploidy = self._ploidy[sl]
+        return sub
 
     def dense(self) -> np.ndarray:
         return self.table[self.codes]
 
 
-def kappa_sum(reads: np.ndarray, log_lam: Optional[float]) -> float:
+def kappa_sum(reads, log_lam: Optional[float]) -> float:
     """sum over (bin, cell) of the parameter-free part of the NB log density that the
-    kernels leave out: (x log lam) + (x log x - x) - lgamma(1 + x)."""
-    x = torch.as_tensor(np.asarray(reads), dtype=torch.float64)
+    kernels leave out: (x log lam) + (x log x - x) - lgamma(1 + x), in fp64 on the device of
+    ``reads`` (a tensor: zero padding adds nothing) or on the host (an array)."""
+    return kappa_and_sum(reads, log_lam)[0]
+
+
+def kappa_and_sum(reads, log_lam: Optional[float]):
+    """(kappa_sum, sum of reads), both fp64."""
+    if isinstance(reads, torch.Tensor):
+        x = reads.to(torch.float64)
+    else:
+        x = torch.as_tensor(np.asarray(reads), dtype=torch.float64)
     xlx = torch.where(x > 0, x * torch.log(torch.where(x > 0, x, torch.ones_like(x))), torch.zeros_like(x))
     s = float((xlx - x - torch.lgamma(1.0 + x)).sum())
+    total = float(x.sum())
     if log_lam is not None:
-        s += float(x.sum()) * log_lam
-    return s
+        s += total * log_lam
+    return s, total
 
 
 # --------------------------------------------------------------------------- step-1 pi block
@@ -262,10 +297,9 @@ class PertShard:
         self.ldn = ldn = -(-NS // nat.BLOCK) * nat.BLOCK      # row stride: stored columns rounded up to 256
 
         # ---- inputs (pert_model.py:133-191 layouts)
-        self.reads = self._pad_rows(torch.as_tensor(reads.astype(F32)), dev)
+        self.reads = self._pad_rows(torch.as_tensor(np.ascontiguousarray(reads, dtype=F32)), dev)
         self.gcf = gc_features(gc, self.K).to(dev).contiguous()
         self.libs = torch.as_tensor(np.asarray(libs).astype(np.int32), device=dev)
-        x64 = reads.astype(np.float64)
         mean_reads = torch.mean(torch.as_tensor(reads, dtype=torch.float32), dim=0)
         if self.paired:
             mean_reads = torch.cat([mean_reads, mean_reads])
@@ -277,7 +311,7 @@ class PertShard:
                 raise ValueError("steps 2/3 need the CN prior eta")
             if eta.P != self.P or eta.codes.shape != (L, N):
                 raise ValueError("eta code book does not match (L, N, P)")
-            ploidy = torch.mean(torch.as_tensor(eta.argmax_states(), dtype=torch.float32), dim=0).numpy()  # :591-593
+            ploidy = eta.ploidy()                                                      # :591-593
         self.ploidy = torch.as_tensor(ploidy, dtype=torch.float32, device=dev)
 
         self.eta = eta
@@ -333,13 +367,18 @@ class PertShard:
         self.pass_events = None      # list -> (start, end) HIP events around every pass
 
         # ---- constants of the loss (added on the host, summed over ranks once)
+        # (fp64 on the device, from the padded reads already there: zero columns add nothing)
         if self.kind == nat.KIND_STEP1:
             copies = 2 if self.paired else 1
-            const = copies * kappa_sum(x64, None) + L * N * math.lgamma(self.P)   # Dirichlet(ones) normaliser
-            self.sum_reads = copies * float(x64.sum())
+            kap, tot = kappa_and_sum(self.reads, None)
+            const = copies * kap + L * N * math.lgamma(self.P)   # Dirichlet(ones) normaliser
+            self.sum_reads = copies * tot
             self.pi_block = CanonicalPiBlock(self.P, self.lr, self.betas, self.eps)
         else:
-            const = kappa_sum(x64, math.log(lam_f)) + eta.dirichlet_normaliser(dirichlet_mode)
+            # code counts from the device copy of the codes (int16 view of uint16)
+            cnt = torch.bincount((self.eta_code[:, :N].to(torch.int32) & 0xFFFF).reshape(-1),
+                                 minlength=int(eta.table.shape[0])).cpu().numpy()
+            const = kappa_sum(self.reads, math.log(lam_f)) + eta.dirichlet_normaliser(dirichlet_mode, counts=cnt)
             self.sum_reads = 0.0
             self.pi_block = None
         c = torch.tensor([const], dtype=torch.float64, device=dev)
@@ -378,10 +417,11 @@ class PertShard:
 
     # ------------------------------------------------------------------ layouts
     def _pad_rows(self, a: torch.Tensor, dev) -> torch.Tensor:
-        """(L, N) -> (L, ldn) zero-padded device copy (include/pert_hip.h row stride)."""
-        out = torch.zeros((a.shape[0], self.ldn), dtype=a.dtype)
-        out[:, :a.shape[1]] = a
-        return out.to(dev).contiguous()
+        """(L, N) -> (L, ldn) zero-padded device copy (include/pert_hip.h row stride): the
+        compact array is copied to the device and padded there."""
+        out = torch.zeros((a.shape[0], self.ldn), dtype=a.dtype, device=dev)
+        out[:, :a.shape[1]] = a.to(dev)
+        return out
 
     def to_tiles(self, a: torch.Tensor) -> torch.Tensor:
         """(L, N, P) -> wave tiles (ldn/64, L, P, 64) on the device."""

@@ -34,7 +34,7 @@ def init_params(kind: int, reads: Optional[np.ndarray], libs: np.ndarray, n_libs
     (the values are the same; step 1's doubled cells need not be materialised)."""
     if mean_reads is None:
         L, N = reads.shape
-        mean_reads = reads.astype(np.float64).mean(0)
+        mean_reads = np.mean(reads, axis=0, dtype=np.float64)      # = reads.astype(float64).mean(0), no copy
     else:
         L, N = int(n_bins), int(np.asarray(mean_reads).shape[0])
     K1 = K + 1

@@ -385,7 +385,7 @@ class pert_infer_scRT():
         s0, s1 = dd.bounds(N)
         sl = slice(s0, s1)
         if eta is not None:
-            eta = EtaCodebook(np.ascontiguousarray(eta.codes[:, sl]), eta.table)
+            eta = eta.cells(sl)
         for k in ("cn_obs", "rep_obs"):
             if k in kw:
                 kw[k] = np.asarray(kw[k])[:, sl]
@@ -482,7 +482,7 @@ class pert_infer_scRT():
             # ---- step 1: G1/2 cells doubled, cn / rep observed (:718-774)
             # the doubled training set (make_g1_g2_training_data, :228-251) in pair mode: the
             # G1/2 columns stored once, rep 0 / rep 1 copies as cells [0, NG) / [NG, 2 NG)
-            mean_g = inp.reads_g.astype(np.float64).mean(0)
+            mean_g = np.mean(inp.reads_g, axis=0, dtype=np.float64)
             lb_g2 = np.concatenate([inp.libs_g, inp.libs_g])
             init1 = init_params(KIND_STEP1, None, lb_g2, n_libs, P, K, seed=self.seed, method=self.init_method,
                                 mean_reads=np.concatenate([mean_g, mean_g]), n_bins=inp.reads_g.shape[0])
@@ -507,7 +507,7 @@ class pert_infer_scRT():
             mark("wait_priors")
             # (the helper runs its tasks in order: the two tau initialisers never share the pool)
             fut_prep3 = helper.submit(on_device, self._prep_step3, inp, profiles) if self.run_step3 else None
-            ploidy = etas.argmax_states().astype(np.float32).mean(0)
+            ploidy = etas.ploidy()
             init2 = init_params(KIND_STEP2, inp.reads_s, inp.libs_s, n_libs, P, K, ploidy=ploidy, t_init=t_init,
                                 beta_means=beta_means_fit, seed=self.seed, method=self.init_method)
             s2 = self._shard(KIND_STEP2, dd, inp.reads_s, inp.libs_s, init2, eta=etas, lamb=float(lambda_fit[0]),
@@ -534,7 +534,7 @@ class pert_infer_scRT():
                 tic = time.perf_counter()
                 etas2, t_init2 = fut_prep3.result()
                 self.t_init_g = t_init2
-                ploidy2 = etas2.argmax_states().astype(np.float32).mean(0)
+                ploidy2 = etas2.ploidy()
                 self.timings["prep_step3"] = time.perf_counter() - tic      # the part step 2 did not hide
                 init3 = init_params(KIND_STEP3, inp.reads_g, inp.libs_g, n_libs, P, K, ploidy=ploidy2,
                                     t_init=t_init2, beta_means=beta_means_fit, seed=self.seed, method=self.init_method)

@@ -367,18 +367,21 @@ class PertShard:
         self.pass_events = None      # list -> (start, end) HIP events around every pass
 
         # ---- constants of the loss (added on the host, summed over ranks once)
-        # (fp64 on the device, from the padded reads already there: zero columns add nothing)
+        # (fp64 on the device, from the padded reads already there: zero columns add nothing; a
+        # small shard on the host, where the device's first lgamma launch would cost more)
+        big = L * NS >= 4_000_000
+        src = self.reads if big else np.asarray(reads)
         if self.kind == nat.KIND_STEP1:
             copies = 2 if self.paired else 1
-            kap, tot = kappa_and_sum(self.reads, None)
+            kap, tot = kappa_and_sum(src, None)
             const = copies * kap + L * N * math.lgamma(self.P)   # Dirichlet(ones) normaliser
             self.sum_reads = copies * tot
             self.pi_block = CanonicalPiBlock(self.P, self.lr, self.betas, self.eps)
         else:
             # code counts from the device copy of the codes (int16 view of uint16)
-            cnt = torch.bincount((self.eta_code[:, :N].to(torch.int32) & 0xFFFF).reshape(-1),
-                                 minlength=int(eta.table.shape[0])).cpu().numpy()
-            const = kappa_sum(self.reads, math.log(lam_f)) + eta.dirichlet_normaliser(dirichlet_mode, counts=cnt)
+            cnt = (torch.bincount((self.eta_code[:, :N].to(torch.int32) & 0xFFFF).reshape(-1),
+                                  minlength=int(eta.table.shape[0])).cpu().numpy() if big else None)
+            const = kappa_sum(src, math.log(lam_f)) + eta.dirichlet_normaliser(dirichlet_mode, counts=cnt)
             self.sum_reads = 0.0
             self.pi_block = None
         c = torch.tensor([const], dtype=torch.float64, device=dev)

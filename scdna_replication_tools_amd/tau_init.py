@@ -728,7 +728,7 @@ def exact_scan(x: np.ndarray, mean_0, mean_1, MEAN_GAP=MEAN_GAP_THRESH, EARLY=EA
     return cell_rt.sum() / len(cell_rt)
 
 
-def exact_fractions(norm_cols: np.ndarray, labels=None, n_threads: int = 1, chunk: int = 32) -> np.ndarray:
+def exact_fractions(norm_cols: np.ndarray, labels=None, n_threads: int = 1, chunk: int = None) -> np.ndarray:
     """The reference's replicated fraction (manhattan_binarization, pert_model.py:364-423)
     of every column of ``norm_cols`` (L, n) fp32 (the CN-normalised reads), bit for bit:
     standardisation, k-means labels (``labels`` (n, L) where the batched pass has settled
@@ -752,6 +752,10 @@ def exact_fractions(norm_cols: np.ndarray, labels=None, n_threads: int = 1, chun
         for j in range(hi - lo):
             out[lo + j] = exact_scan(Xs[j], mu[j, 0], mu[j, 1], distinct=(dist[0][j], dist[1][j]))
 
+    if chunk is None:
+        # large chunks: the EM runs batched over a chunk, and its per-iteration Python work (which
+        # holds the GIL the threads share) is paid once per chunk, not once per cell
+        chunk = max(32, min(128, -(-n // max(1, n_threads))))
     spans = [(i, min(n, i + chunk)) for i in range(0, n, chunk)]
     if n_threads <= 1 or len(spans) == 1:
         for lo, hi in spans:

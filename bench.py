@@ -412,7 +412,7 @@ def main():
         bpc = 2.5 if step1 else bytes_per_cellbin(P)
         local_cb = L * (n1 - n0) * (2 if step1 else 1)
         achieved = bpc * local_cb / (kern_ms * 1e-3) / 1e9
-        kname = ("obs_kernel" if step1 else
+        kname = ("obs_pair_kernel<5>" if step1 else
                  "enum3_kernel<13, 0, 5>" if args.variant == 3 else
                  "enum_dma_kernel<13, 0, 5>")
         traffic, valu = None, None

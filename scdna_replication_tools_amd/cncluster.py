@@ -39,6 +39,23 @@ def compute_bic(centers: np.ndarray, labels: np.ndarray, X: np.ndarray) -> float
     return float(np.sum(terms) - const_term)
 
 
+def compute_bic_tensor(centers: torch.Tensor, labels: torch.Tensor, X: torch.Tensor) -> float:
+    """compute_bic on the tensors' device, fp64 (the same formula; only the order of the sum
+    of squares differs from numpy's)."""
+    X = X.to(torch.float64)
+    centers = centers.to(torch.float64)
+    n_clusters = centers.shape[0]
+    sizes = torch.bincount(labels, minlength=n_clusters).to(torch.float64)
+    N, d = X.shape
+    sq = float(((X - centers[labels]) ** 2).sum())
+    cl_var = (1.0 / (N - n_clusters) / d) * sq
+    const_term = 0.5 * n_clusters * np.log(N) * (d + 1)
+    sz = sizes.cpu().numpy()
+    with np.errstate(divide="ignore", invalid="ignore"):
+        terms = (sz * np.log(sz) - sz * np.log(N) - ((sz * d) / 2) * np.log(2 * np.pi * cl_var) - ((sz - 1) * d / 2))
+    return float(np.sum(terms) - const_term)
+
+
 def _sq_dist(X: torch.Tensor, xx: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
     """||x - c||^2 for every (restart, point, centre): (R, N, k), clamped at 0."""
     cc = (C * C).sum(-1)                                           # (R, k)
@@ -100,15 +117,25 @@ def kmeans_fit(X: np.ndarray, k: int, n_init: int = 10, random_state: int = 0, d
     """One KMeans(n_clusters=k, init='k-means++', n_init=n_init) fit: (centres, labels, inertia)
     of the restart with the least inertia."""
     dev = torch.device(device) if device is not None else torch.device("cuda" if torch.cuda.is_available() else "cpu")
-    Xt = torch.as_tensor(np.asarray(X, dtype=np.float64), device=dev)
-    tol = 1e-4 * float(Xt.var(0, unbiased=False).mean())
-    xx = (Xt * Xt).sum(1)
+    C, lab, inertia = _kmeans_fit_tensor(torch.as_tensor(np.asarray(X, dtype=np.float64), device=dev), k, n_init,
+                                         random_state, max_iter)
+    return C.cpu().numpy(), lab.cpu().numpy(), inertia
+
+
+def _kmeans_fit_tensor(Xt: torch.Tensor, k: int, n_init: int, random_state: int, max_iter: int = 300, tol=None,
+                       xx=None):
+    """kmeans_fit on a device tensor: (centres, labels) tensors and the inertia."""
+    dev = Xt.device
+    if tol is None:
+        tol = 1e-4 * float(Xt.var(0, unbiased=False).mean())
+    if xx is None:
+        xx = (Xt * Xt).sum(1)
     gen = torch.Generator(device=dev)
     gen.manual_seed(int(random_state) * 1000003 + k)
     C0 = _kmeans_pp(Xt, xx, k, n_init, gen)
     C, lab, inertia = _lloyd(Xt, xx, C0, tol, max_iter)
     b = int(inertia.argmin())
-    return C[b].cpu().numpy(), lab[b].cpu().numpy(), float(inertia[b])
+    return C[b], lab[b], float(inertia[b])
 
 
 def kmeans_cluster(cn: pd.DataFrame, min_k: int = 2, max_k: int = 100, n_init: int = 10, random_state: int = 0,
@@ -119,6 +146,21 @@ def kmeans_cluster(cn: pd.DataFrame, min_k: int = 2, max_k: int = 100, n_init: i
     X = np.asarray(cn.T.values, dtype=np.float64)
     ks = range(min_k, min(max_k, X.shape[0] - 1) + 1)
     best = None
+    if backend == "device":
+        # the matrix goes to the device once; every k's fit and BIC run there
+        dev = torch.device(device) if device is not None else torch.device(
+            "cuda" if torch.cuda.is_available() else "cpu")
+        Xt = torch.as_tensor(X, device=dev)
+        tol = 1e-4 * float(Xt.var(0, unbiased=False).mean())
+        xx = (Xt * Xt).sum(1)
+        for k in ks:
+            C, lab, _ = _kmeans_fit_tensor(Xt, k, n_init, random_state, tol=tol, xx=xx)
+            bic = compute_bic_tensor(C, lab, Xt)
+            log.info("k=%d bic=%.6g", k, bic)
+            if best is None or bic > best[0]:              # first maximum, like np.argmax
+                best = (bic, k, lab)
+        log.info("selected k=%d", best[1])
+        return pd.DataFrame({"cell_id": cn.columns, "cluster_id": best[2].cpu().numpy()})
     for k in ks:
         if backend == "sklearn":
             import sklearn.cluster

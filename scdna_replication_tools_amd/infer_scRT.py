@@ -22,12 +22,25 @@ def assign_s_to_clones(s_phase_cells: pd.DataFrame, clone_df: pd.DataFrame, col_
                        clone_col='clone_id', cell_col='cell_id', chr_col='chr', start_col='start'):
     """assign_s_to_clones.py:49-79: every S cell gets the clone whose consensus profile
     has the highest Pearson r with the cell's ``col_name`` over the shared loci."""
+    # per-cell blocks (the concatenated per-cell tables of the tutorials): the pivot is a
+    # transpose of the blocks and every row's cell is its block's -- no per-row hashing
+    lay = prep._block_layout(s_phase_cells, cell_col, chr_col, start_col, col_name)
     s = s_phase_cells.copy()
     s[chr_col] = s[chr_col].astype(str)
     clone_df = clone_df.copy()
     if set([chr_col, start_col]).issubset(set(clone_df.columns)):
         clone_df = clone_df.set_index([chr_col, start_col])
-    piv = prep.pivot_cells_by_loci(s, col_name, cell_col, chr_col, start_col)
+    row_cell = None
+    if lay is not None:
+        B, L, bp, q, ch0 = lay
+        cells = np.ascontiguousarray(s[cell_col].to_numpy())[::L][bp]
+        piv = prep.Pivot(cells, np.array(prep.CHR_ORDER, dtype=object)[ch0[q]], s[start_col].to_numpy()[:L][q],
+                         prep._block_pivot(s[col_name].to_numpy(), B, L, bp, q))
+        pos = np.empty(B, np.int64)
+        pos[bp] = np.arange(B)                     # block (table order) -> sorted cell index
+        row_cell = np.repeat(pos, L)
+    else:
+        piv = prep.pivot_cells_by_loci(s, col_name, cell_col, chr_col, start_col)
     cidx = pd.MultiIndex.from_arrays([clone_df.index.get_level_values(0).astype(str),
                                       clone_df.index.get_level_values(1)])
     li = cidx.get_indexer(pd.MultiIndex.from_arrays([piv.loci_chr.astype(str), piv.loci_start]))
@@ -47,9 +60,35 @@ def assign_s_to_clones(s_phase_cells: pd.DataFrame, clone_df: pd.DataFrame, col_
         # Series.argmax (:71): first maximum, NaN skipped; all NaN (a constant profile) gives
         # -1 in the pandas the reference ran on, i.e. the last clone
         best.append(clone_df.columns[int(np.nanargmax(r)) if np.isfinite(r).any() else -1])
-    lut = dict(zip(piv.cells, best))
-    s[clone_col] = s[cell_col].astype(str).map(lut)
+    if row_cell is not None:
+        s[clone_col] = pd.Series(np.asarray(best, dtype=object)[row_cell], index=s.index).infer_objects()
+    else:
+        lut = dict(zip(piv.cells, best))
+        s[clone_col] = s[cell_col].astype(str).map(lut)
     return s
+
+
+def consensus_profiles(cn_g1: pd.DataFrame, col_name, clone_col='clone_id', cell_col='cell_id', chr_col='chr',
+                       start_col='start', cn_state_col='state') -> pd.DataFrame:
+    """compute_consensus_clone_profiles (infer_scRT.py:140-141) of the G1/2 table.  A per-cell
+    block table is sorted by (cell, chr, start) with one gather per column into a temporary copy
+    (the caller's table keeps its row order) and handed over with its RegularKeys, which takes
+    the consensus' block path (no per-row hashing of the labels, identical result)."""
+    lay = prep._block_layout(cn_g1, cell_col, chr_col, start_col, None)
+    if lay is not None and cn_state_col is not None and cn_state_col in cn_g1.columns:
+        out, keys, _, _ = prep._block_table(cn_g1, lay, None, col_name, cn_state_col, cell_col, chr_col, start_col)
+        prof = prep.consensus_clone_profiles(out, col_name, clone_col=clone_col, cell_col=cell_col, chr_col=chr_col,
+                                             start_col=start_col, cn_state_col=cn_state_col, keys=keys)
+        if not isinstance(cn_g1[chr_col].dtype, pd.CategoricalDtype):
+            # the caller's chromosome labels (not the sorted copy's categories), sorted as
+            # pivot_table sorts them
+            idx = prof.index
+            prof.index = pd.MultiIndex.from_arrays(
+                [np.asarray(idx.get_level_values(0), dtype=object), idx.get_level_values(1)], names=idx.names)
+            prof = prof.sort_index()
+        return prof
+    return prep.consensus_clone_profiles(cn_g1, col_name, clone_col=clone_col, cell_col=cell_col, chr_col=chr_col,
+                                         start_col=start_col, cn_state_col=cn_state_col)
 
 
 class scRT:
@@ -124,7 +163,7 @@ class scRT:
         assign_col, S-phase cells assigned to clones, then the PERT model object."""
         if self.clone_col is None:
             # no clone labels: KMeans + BIC over the G1/2 cells' assign_col profiles (:129-138)
-            piv = prep.pivot_cells_by_loci(self.cn_g1, self.assign_col, self.cell_col, self.chr_col, self.start_col)
+            piv = prep.pivot_any(self.cn_g1, self.assign_col, self.cell_col, self.chr_col, self.start_col)
             g1_mat = pd.DataFrame(piv.values, columns=pd.Index(piv.cells, name=self.cell_col),
                                   index=pd.MultiIndex.from_arrays([piv.loci_chr, piv.loci_start],
                                                                   names=[self.chr_col, self.start_col]))
@@ -136,7 +175,7 @@ class scRT:
             self.cn_g1 = self.cn_g1[self.cn_g1["cluster_id"].notna()]
             self.cn_g1["cluster_id"] = self.cn_g1["cluster_id"].astype(np.int64)
             self.clone_col = 'cluster_id'
-        self.clone_profiles = prep.consensus_clone_profiles(
+        self.clone_profiles = consensus_profiles(
             self.cn_g1, self.assign_col, clone_col=self.clone_col, cell_col=self.cell_col, chr_col=self.chr_col,
             start_col=self.start_col, cn_state_col=self.cn_state_col)
         self.cn_s = assign_s_to_clones(self.cn_s, self.clone_profiles, col_name=self.assign_col,

@@ -594,6 +594,18 @@ def _block_pivot(v: np.ndarray, B: int, L: int, bp: np.ndarray, q: np.ndarray) -
     return out
 
 
+def pivot_any(cn: pd.DataFrame, value_col: str, cell_col: str, chr_col: str, start_col: str) -> Pivot:
+    """pivot_cells_by_loci, through the block transpose when the table is per-cell blocks with no
+    missing value (the same sorted cells, loci and values), else the general path."""
+    lay = _block_layout(cn, cell_col, chr_col, start_col, value_col)
+    if lay is None:
+        return pivot_cells_by_loci(cn, value_col, cell_col, chr_col, start_col)
+    B, L, bp, q, ch0 = lay
+    cells = np.ascontiguousarray(cn[cell_col].to_numpy())[::L][bp]
+    vals = _block_pivot(cn[value_col].to_numpy(), B, L, bp, q).astype(np.float64, copy=False)
+    return Pivot(cells, np.array(CHR_ORDER, dtype=object)[ch0[q]], cn[start_col].to_numpy()[:L][q], vals)
+
+
 def _block_table(cn, lay, hook, input_col, cn_state_col, cell_col, chr_col, start_col):
     """process_input_data's per-table work for a per-cell-block table (_block_layout): the
     table sorted by (cell, chr, start) with one gather per column (the cell and chromosome

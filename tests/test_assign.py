@@ -148,3 +148,22 @@ def test_assign_tied_correlations_take_first_clone():
     s = _cells(prof, loci, 12, rng, ["A", "B"], inf_nan=False)
     got = _compare(s, prof)
     assert "C" not in set(got["clone_id"])
+
+
+@pytest.mark.parametrize("ids", [["A", "B", "C"], [0, 1, 2]])
+def test_assign_per_cell_block_table_matches_reference_loop(ids):
+    """The per-cell-block table of the tutorials (each cell's rows contiguous, the same loci in
+    every cell): the block-transpose pivot gives the reference loop's assignment for every row
+    and the same column dtype as the general path (rows shuffled)."""
+    from scdna_replication_tools_amd import prep
+    rng = np.random.default_rng(11)
+    loci = _loci()
+    prof = _clones(ids, loci, rng)
+    s = _cells(prof, loci, 30, rng, ids, inf_nan=False)
+    s = s.sort_values(["cell_id", "chr", "start"], kind="stable").reset_index(drop=True)
+    s["cell_id"] = s["cell_id"].map({c: c for c in s["cell_id"].unique()})   # one str object per cell
+    assert prep._block_layout(s, "cell_id", "chr", "start", "copy") is not None
+    got = _compare(s, prof)
+    general = assign_s_to_clones(s.sample(frac=1.0, random_state=3).reset_index(drop=True), prof.copy(),
+                                 col_name="copy")
+    assert got["clone_id"].dtype == general["clone_id"].dtype

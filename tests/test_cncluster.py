@@ -8,7 +8,7 @@ import pandas as pd
 import pytest
 
 from scdna_replication_tools_amd import prep
-from scdna_replication_tools_amd.cncluster import compute_bic, kmeans_cluster, kmeans_fit
+from scdna_replication_tools_amd.cncluster import compute_bic, compute_bic_tensor, kmeans_cluster, kmeans_fit
 from scdna_replication_tools_amd.simulator import simulate, to_long_form
 
 
@@ -27,11 +27,17 @@ def _bic_loop(centers, labels, X):
 
 
 def test_bic_matches_reference_formula():
+    """Both BIC implementations (host numpy, and the device-tensor one kmeans_cluster uses)
+    against the reference's per-cluster loop."""
+    import torch
     rng = np.random.default_rng(0)
     X = np.concatenate([rng.normal(m, 0.3, size=(40, 7)) for m in (0.0, 2.0, 5.0)])
     for k in (2, 3, 5):
         centers, labels, _ = kmeans_fit(X, k, n_init=4, device="cpu")
-        assert np.isclose(compute_bic(centers, labels, X), float(_bic_loop(centers, labels, X)), rtol=1e-10)
+        ref = float(_bic_loop(centers, labels, X))
+        assert np.isclose(compute_bic(centers, labels, X), ref, rtol=1e-10)
+        got = compute_bic_tensor(torch.as_tensor(centers), torch.as_tensor(labels), torch.as_tensor(X))
+        assert np.isclose(got, ref, rtol=1e-10)
 
 
 def _g1_matrix(n=60, L=400, seed=3):

@@ -228,3 +228,29 @@ def test_block_path_keys_serve_every_consumer():
     p1 = prep.pivot_cells_by_loci(cn_g1, "reads", "cell_id", "chr", "start", inp.keys_g)
     p2 = prep.pivot_cells_by_loci(cn_g1, "reads", "cell_id", "chr", "start")
     np.testing.assert_array_equal(p1.values, p2.values)
+
+
+def test_scrt_consensus_block_path_equals_general_path():
+    """infer_scRT.consensus_profiles (a per-cell block table sorted into a temporary copy with
+    RegularKeys) returns the general path's profiles exactly: index, columns, dtypes, values."""
+    from scdna_replication_tools_amd.infer_scRT import consensus_profiles
+    from scdna_replication_tools_amd.simulator import simulate, to_long_form
+    sim = simulate(n_s=4, n_g=90, n_bins=400, num_reads=400 * 183, seed=4, n_clones=3)
+    _, df_g = to_long_form(sim, n_libs=1, copy_from="reads")
+    assert prep._block_layout(df_g, "cell_id", "chr", "start", None) is not None
+    for col in ("copy", "state"):
+        a = prep.consensus_clone_profiles(df_g, col, clone_col="clone_id", cn_state_col="state")
+        b = consensus_profiles(df_g, col, clone_col="clone_id", cn_state_col="state")
+        pd.testing.assert_frame_equal(a, b)
+
+
+def test_pivot_any_block_path_equals_general_pivot():
+    from scdna_replication_tools_amd.simulator import simulate, to_long_form
+    sim = simulate(n_s=4, n_g=30, n_bins=300, num_reads=300 * 183, seed=6)
+    _, df_g = to_long_form(sim, n_libs=1, copy_from="reads")
+    for col in ("copy", "reads", "state"):
+        a = prep.pivot_cells_by_loci(df_g, col, "cell_id", "chr", "start")
+        b = prep.pivot_any(df_g, col, "cell_id", "chr", "start")
+        assert list(a.cells) == list(b.cells) and list(a.loci_chr) == list(b.loci_chr)
+        np.testing.assert_array_equal(a.loci_start, b.loci_start)
+        np.testing.assert_array_equal(np.asarray(a.values, np.float64), np.asarray(b.values, np.float64))

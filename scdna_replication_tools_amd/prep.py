@@ -584,13 +584,25 @@ def _block_pivot(v: np.ndarray, B: int, L: int, bp: np.ndarray, q: np.ndarray) -
     (``bp``), loci in (chr, start) order (``q``) -- a transpose of the blocks.  Integer
     columns whose values fp32 holds exactly come as float32 (the int64-truncated fp32 tensor
     of pert_model.py:163-166 itself), others as float64."""
+    from concurrent.futures import ThreadPoolExecutor
     g = np.asarray(v).reshape(B, L)
-    g = g[bp] if not np.array_equal(bp, np.arange(B)) else g
-    if not np.array_equal(q, np.arange(L)):
-        g = g[:, q]
-    exact32 = g.dtype.kind in "iu" and (g.size == 0 or (g.min() > -(1 << 24) and g.max() < (1 << 24)))
-    out = np.empty((L, B), dtype=np.float32 if exact32 else np.float64)
-    out[...] = g.T
+    same_b, same_q = np.array_equal(bp, np.arange(B)), np.array_equal(q, np.arange(L))
+    # cell tiles on a few threads (numpy's gathers, reductions and casting copies release the
+    # GIL): one gather + transpose + cast per tile, instead of a strided whole-matrix copy
+    T = 64
+    starts = range(0, B, T)
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        exact32 = g.dtype.kind in "iu"
+        if exact32 and g.size:
+            mm = list(ex.map(lambda j0: (g[j0:j0 + 4 * T].min(), g[j0:j0 + 4 * T].max()), range(0, B, 4 * T)))
+            exact32 = min(m[0] for m in mm) > -(1 << 24) and max(m[1] for m in mm) < (1 << 24)
+        out = np.empty((L, B), dtype=np.float32 if exact32 else np.float64)
+
+        def tile(j0):
+            j1 = min(B, j0 + T)
+            t = g[j0:j1] if same_b else g[bp[j0:j1]]
+            out[:, j0:j1] = (t if same_q else t[:, q]).T
+        list(ex.map(tile, starts))
     return out
 
 

@@ -630,7 +630,17 @@ def _block_table(cn, lay, hook, input_col, cn_state_col, cell_col, chr_col, star
     loci_start = cn[start_col].to_numpy()[:L][q]
     order = (bp.astype(np.int64)[:, None] * L + q[None, :]).reshape(-1)
     chr_cat = pd.Categorical.from_codes(np.tile(chq.astype(np.int8), B), categories=CHR_ORDER)
-    out = _take_columns(cn, order, replace={cell_col: np.repeat(cells.astype(object), L), chr_col: chr_cat})
+    replace = {cell_col: np.repeat(cells.astype(object), L), chr_col: chr_cat}
+    for name in cn.columns:
+        # per-cell label columns (library, clone): one object per block, by identity -- the
+        # block heads repeated instead of a gather of every row
+        if name in replace or name == cell_col or cn[name].dtype != object:
+            continue
+        a = np.ascontiguousarray(cn[name].to_numpy())
+        p2 = _object_pointers(a).reshape(B, L)
+        if (p2 == p2[:, :1]).all():
+            replace[name] = np.repeat(a[::L][bp], L)
+    out = _take_columns(cn, order, replace=replace)
     k = RegularKeys(cells, loci_chr, loci_start, L)
     if hook is not None:
         hook(out, k)

@@ -21,7 +21,8 @@ def _table(n_cells=7, prefix="c", seed=0, chroms=("1", "2", "10", "X"), per_chr=
                 rows.append(dict(cell_id="{}{}".format(prefix, (i * 7919) % 1000), chr=ch, start=j * 500000 + 1,
                                  gc=0.3 + 0.01 * j + 0.001 * CHR.index(ch), library_id="L{}".format(i % n_libs),
                                  state=int(rng.integers(1, 5)), reads=float(rng.integers(0, 300)),
-                                 clone_id="AB"[i % 2], copy=float(rng.uniform(1, 4))))
+                                 clone_id="AB"[i % 2], copy=float(rng.uniform(1, 4)),
+                                 note="n{}".format(j % 3)))         # a label that varies within a cell
     df = pd.DataFrame(rows)
     if order == "shuffled":
         df = df.sample(frac=1.0, random_state=seed).reset_index(drop=True)
@@ -45,7 +46,7 @@ def _table(n_cells=7, prefix="c", seed=0, chroms=("1", "2", "10", "X"), per_chr=
     if shared:
         # one Python object per distinct label (as np.repeat-built or CSV-parsed tables hold
         # them): the per-cell block layout is then recognised from object identity
-        for c in ("cell_id", "chr", "library_id", "clone_id"):
+        for c in ("cell_id", "chr", "library_id", "clone_id", "note"):
             canon = {}
             df[c] = pd.Series([canon.setdefault(v, v) for v in df[c].tolist()], dtype=object)
     return df

@@ -607,8 +607,8 @@ class pert_infer_scRT():
             base = cn_s
             L = len(loci_start)
             model = {
-                'model_cn_state': np.ascontiguousarray(model_cn.T).reshape(-1).astype(np.int64),
-                'model_rep_state': np.ascontiguousarray(model_rep.T).reshape(-1).astype(np.float32),
+                'model_cn_state': prep.transpose_cast(model_cn, np.int64).reshape(-1),
+                'model_rep_state': prep.transpose_cast(model_rep, np.float32).reshape(-1),
                 'model_tau': np.repeat(per_cell("expose_tau"), L),
                 'model_u': np.repeat(per_cell("expose_u"), L),
                 'model_rho': np.tile(per_cell("expose_rho"), len(cells)),

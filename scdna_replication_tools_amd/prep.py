@@ -606,6 +606,23 @@ def _block_pivot(v: np.ndarray, B: int, L: int, bp: np.ndarray, q: np.ndarray) -
     return out
 
 
+def transpose_cast(a: np.ndarray, dtype) -> np.ndarray:
+    """``np.ascontiguousarray(a.T).astype(dtype)`` for a (loci x cells) matrix: the (cells x
+    loci) rows a long table in (cell, locus) order holds, by cell tiles on a few threads (one
+    transpose + cast per tile, as _block_pivot)."""
+    from concurrent.futures import ThreadPoolExecutor
+    a = np.asarray(a)
+    L, N = a.shape
+    out = np.empty((N, L), dtype=dtype)
+    T = 64
+
+    def tile(j0):
+        out[j0:j0 + T] = a[:, j0:j0 + T].T
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        list(ex.map(tile, range(0, N, T)))
+    return out
+
+
 def pivot_any(cn: pd.DataFrame, value_col: str, cell_col: str, chr_col: str, start_col: str) -> Pivot:
     """pivot_cells_by_loci, through the block transpose when the table is per-cell blocks with no
     missing value (the same sorted cells, loci and values), else the general path."""

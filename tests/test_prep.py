@@ -270,3 +270,16 @@ def test_block_pivot_tiles_equal_whole_transpose(kind):
         want = v.reshape(B, L)[bp][:, q].T
         assert got.dtype == (np.float32 if kind == "int" else np.float64)
         np.testing.assert_array_equal(got, want.astype(got.dtype))
+
+
+@pytest.mark.parametrize("shape", [(7, 1), (37, 300), (5, 64), (3, 65), (0, 5), (5, 0)])
+def test_transpose_cast_equals_numpy(shape):
+    """prep.transpose_cast (threaded cell tiles; package_s_output's (cell, locus) columns) is
+    np.ascontiguousarray(a.T).astype(dtype), also for a non-contiguous view."""
+    a = np.random.default_rng(5).integers(0, 13, shape).astype(np.uint8)
+    for dt in (np.int64, np.float32):
+        got = prep.transpose_cast(a, dt)
+        assert got.dtype == dt
+        np.testing.assert_array_equal(got, np.ascontiguousarray(a.T).astype(dt))
+    v = a[:, 1:]
+    np.testing.assert_array_equal(prep.transpose_cast(v, np.int64), v.T.astype(np.int64))

@@ -84,13 +84,16 @@ class EtaCodebook:
 
     @classmethod
     def from_states(cls, states, weight: float, P: int) -> "EtaCodebook":
-        """build_cn_prior (pert_model.py:272-282): ones with eta[state] = weight."""
-        s = np.asarray(states).astype(np.int64)
-        if s.min() < 0 or s.max() >= P:
+        """build_cn_prior (pert_model.py:272-282): ones with eta[state] = weight.  uint16
+        states are taken as the codes themselves (no widening copy)."""
+        s = np.asarray(states)
+        if s.dtype != np.uint16:
+            s = s.astype(np.int64)
+        if s.size and (s.min() < 0 or s.max() >= P):
             raise ValueError("CN states must lie in [0, P) for P={}".format(P))
         table = np.ones((P, P), dtype=F32)
         table[np.arange(P), np.arange(P)] = F32(weight)
-        return cls(s.astype(np.uint16), table)
+        return cls(np.ascontiguousarray(s, dtype=np.uint16), table)
 
     def kernel_table(self) -> np.ndarray:
         """(n_codes, P+1): eta_k - 1, then S1 = sum_k (eta_k - 1) (include/pert_hip.h)."""

@@ -817,10 +817,26 @@ def _consensus_blocks(cn: pd.DataFrame, col_name: str, clone_col: str, cn_state_
         keep &= pc == cc.argmax(axis=1)[np.where(kcell >= 0, kcell, 0)]
     med = np.full((L, len(ku)), np.nan)
     for c in range(len(ku)):
-        rows = keep & (kcell == c)
-        if rows.any():
-            med[:, c] = np.median(vals[rows], axis=0)
+        rows = np.flatnonzero(keep & (kcell == c))
+        if rows.size:
+            med[:, c] = _column_median(vals, rows)
     return med, ku
+
+
+def _column_median(vals: np.ndarray, rows: np.ndarray) -> np.ndarray:
+    """np.median(vals[rows], axis=0) for a (cells, L) matrix: locus tiles on a few threads,
+    each gathered and transposed so the median runs along contiguous rows (np.median of the
+    same values per locus: the same result)."""
+    from concurrent.futures import ThreadPoolExecutor
+    L = vals.shape[1]
+    out = np.empty(L)
+    T = 256
+
+    def tile(l0):
+        out[l0:l0 + T] = np.median(np.ascontiguousarray(vals[rows, l0:l0 + T].T), axis=1)
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        list(ex.map(tile, range(0, L, T)))
+    return out
 
 
 def consensus_clone_profiles(cn: pd.DataFrame, col_name: str, clone_col="clone_id", cell_col="cell_id",
@@ -898,15 +914,21 @@ def first_clone(cn: pd.DataFrame, cells, cell_col="cell_id", clone_col="clone_id
     return f.reindex(cells).to_numpy()
 
 
-def _profile_matrix(profiles: pd.DataFrame, clones, loci_chr, loci_start) -> np.ndarray:
+def _profile_columns(profiles: pd.DataFrame, clones, loci_chr, loci_start):
+    """(the profiles at the fitted loci (L, n_profiles), each cell's profile column (N,))."""
     idx = pd.MultiIndex.from_arrays([profiles.index.get_level_values(0).astype(str),
                                      profiles.index.get_level_values(1)])
     li = idx.get_indexer(pd.MultiIndex.from_arrays([np.asarray(loci_chr).astype(str), loci_start]))
     if (li < 0).any():
         raise ValueError("clone profiles miss some loci of the fitted cells")
     cols = {c: j for j, c in enumerate(profiles.columns)}
-    mat = profiles.to_numpy()[li]
-    return np.stack([mat[:, cols[c]] for c in clones], axis=1)
+    return profiles.to_numpy()[li], np.array([cols[c] for c in clones], dtype=np.int64)
+
+
+def _profile_matrix(profiles: pd.DataFrame, clones, loci_chr, loci_start) -> np.ndarray:
+    """(L, N): each cell's clone profile at the fitted loci (pert_model.py:289-293)."""
+    mat, ci = _profile_columns(profiles, clones, loci_chr, loci_start)
+    return np.take(mat, ci, axis=1)
 
 
 # --------------------------------------------------------------------------- eta builders
@@ -917,10 +939,16 @@ def build_cn_prior(states, weight: float, P: int) -> EtaCodebook:
 
 def build_clone_cn_prior(cn: pd.DataFrame, cells, loci_chr, loci_start, profiles: pd.DataFrame, weight: float,
                          P: int, cell_col="cell_id", clone_col="clone_id", keys=None) -> EtaCodebook:
-    """pert_model.py:285-296: the consensus clone profile (int64-truncated) as prior state."""
+    """pert_model.py:285-296: the consensus clone profile (int64-truncated) as prior state --
+    truncated and range-checked per clone, then one uint16 gather of the clone columns
+    (the same codes as build_cn_prior on the (L, N) profile matrix)."""
     clones = first_clone(cn, cells, cell_col, clone_col, keys)
-    prof = _profile_matrix(profiles, clones, loci_chr, loci_start)
-    return build_cn_prior(prof.astype(np.int64), weight, P)
+    mat, ci = _profile_columns(profiles, clones, loci_chr, loci_start)
+    st = mat.astype(np.int64)
+    used = st[:, np.unique(ci)]
+    if used.size and (used.min() < 0 or used.max() >= P):      # before the uint16 narrowing
+        raise ValueError("CN states must lie in [0, P) for P={}".format(P))
+    return EtaCodebook.from_states(np.take(st.astype(np.uint16), ci, axis=1), weight, P)
 
 
 def pearson_columns(A: np.ndarray, B: np.ndarray) -> np.ndarray:

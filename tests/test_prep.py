@@ -176,6 +176,28 @@ def test_clone_prior_matches_dense_reference():
         np.testing.assert_array_equal(dense[:, n], want)
 
 
+@pytest.mark.parametrize("bad", [13.0, -1.0, 65536.0 + 2.0])
+def test_clone_prior_refuses_out_of_range_states(bad):
+    """A clone profile state outside [0, P) is refused (build_cn_prior's range check), also one
+    that narrowing to the uint16 codes would wrap into range."""
+    s = _table(8, "s", seed=4)
+    g = _table(6, "g", seed=5)
+    cn_s, cn_g1, inp = prep.process_input_data(s, g)
+    prof = prep.consensus_clone_profiles(cn_g1, "state").copy()
+    prof.iloc[3, 0] = bad
+    with pytest.raises(ValueError):
+        prep.build_clone_cn_prior(cn_s, inp.cells_s, inp.loci_chr, inp.loci_start, prof, 1e6, 13)
+
+
+def test_column_median_equals_numpy():
+    """prep._column_median (threaded locus tiles) is np.median(vals[rows], axis=0)."""
+    rng = np.random.default_rng(6)
+    for n, L in [(1, 7), (300, 600), (65, 257)]:
+        for v in (rng.integers(0, 9, (n, L)).astype(np.float64), rng.normal(size=(n, L))):
+            rows = np.sort(rng.choice(n, size=max(1, n // 2), replace=False))
+            np.testing.assert_array_equal(prep._column_median(v, rows), np.median(v[rows], axis=0))
+
+
 def test_consensus_matches_reference_golden():
     """prep.consensus_clone_profiles against the reference's own compute_consensus_clone_profiles
     output (tests/golden/make_reference_golden.py; cn_state_col=None path, unsorted rows,

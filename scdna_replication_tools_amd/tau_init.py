@@ -773,6 +773,26 @@ def default_threads() -> int:
     return max(1, min(16, len(os.sched_getaffinity(0))))
 
 
+def cn_normalise(reads: np.ndarray, cn_states: np.ndarray) -> np.ndarray:
+    """reads / where(state > 0, state, 0.5) in fp32 (pert_model.py:446-448: the states cast to
+    float32, each quotient the correctly rounded fp32 division torch performs), by locus tiles
+    on a few threads."""
+    from concurrent.futures import ThreadPoolExecutor
+    x = np.asarray(reads, np.float32)
+    st = np.asarray(cn_states)
+    if x.shape != st.shape or x.ndim != 2:
+        raise ValueError("reads and CN states must be (loci, cells) of one shape")
+    out = np.empty(x.shape, np.float32)
+    T = 256
+
+    def tile(l0):
+        s = st[l0:l0 + T].astype(np.float32)
+        np.divide(x[l0:l0 + T], np.where(s > 0.0, s, np.float32(0.5)), out=out[l0:l0 + T])
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        list(ex.map(tile, range(0, x.shape[0], T)))
+    return out
+
+
 def guess_times_batched(reads: np.ndarray, cn_states: np.ndarray, upsilon: float = 6, device=None,
                         n_threads: int = None):
     """pert_model.py:426-457: (t_init, t_alpha_prior, t_beta_prior), all cells at once.
@@ -782,11 +802,9 @@ def guess_times_batched(reads: np.ndarray, cn_states: np.ndarray, upsilon: float
     every cell's t_init is the reference's.  No worker processes."""
     t0 = time.perf_counter()
     dev = torch.device(device) if device is not None else torch.device("cpu")
-    x = torch.as_tensor(np.asarray(reads, np.float32))
-    st = torch.as_tensor(np.asarray(cn_states, np.float32))
     # the reference's normalisation (:446-448), on the host in fp32 (these are the values
     # the exact path standardises); the batched pass reads the same values on the device
-    norm = x / torch.where(st > 0.0, st, (torch.ones(x.shape) * 0.5).type(torch.float32))
+    norm = torch.from_numpy(cn_normalise(reads, cn_states))
     frac, lab_unsure, near, lab = binarization_fraction(norm.to(dev), return_fragile=True, return_minor=True)
     t = frac.to(torch.float32).cpu().numpy()
     redo = np.flatnonzero((lab_unsure | near).cpu().numpy())
@@ -803,7 +821,7 @@ def guess_times_batched(reads: np.ndarray, cn_states: np.ndarray, upsilon: float
         guess_times_batched.last_kmeans = 0
     guess_times_batched.last_fragile = redo
     guess_times_batched.last_timings = {"batched_s": t1 - t0, "exact_s": time.perf_counter() - t1,
-                                        "cells": int(x.shape[1]), "exact_cells": int(redo.size),
+                                        "cells": int(norm.shape[1]), "exact_cells": int(redo.size),
                                         "kmeans_cells": guess_times_batched.last_kmeans}
     alpha = (t * np.float32(upsilon)).astype(np.float32)
     return t, alpha, (np.float32(upsilon) - alpha).astype(np.float32)

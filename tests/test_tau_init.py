@@ -151,3 +151,18 @@ def test_host_helper_equals_numpy_restatement():
     labs = np.stack([tau_init.exact_kmeans_labels(Xs[j]) for j in range(Xs.shape[0])])
     np.testing.assert_array_equal(tau_init.exact_gmm_means(Xs, labs, use_host=True),
                                   tau_init.exact_gmm_means(Xs, labs, use_host=False))
+
+
+def test_cn_normalise_equals_reference_expression():
+    """tau_init.cn_normalise (threaded locus tiles) gives the bits of pert_model.py:446-448's
+    torch expression, zero / negative / NaN states included."""
+    import torch
+    rng = np.random.default_rng(11)
+    reads = rng.integers(0, 400, (600, 37)).astype(np.float32)
+    states = rng.integers(-1, 7, (600, 37)).astype(np.float64)
+    states[3, 4] = np.nan
+    x, st = torch.as_tensor(reads), torch.as_tensor(states.astype(np.float32))
+    want = (x / torch.where(st > 0.0, st, (torch.ones(x.shape) * 0.5).type(torch.float32))).numpy()
+    got = tau_init.cn_normalise(reads, states)
+    assert got.dtype == np.float32
+    np.testing.assert_array_equal(got.view(np.int32), want.view(np.int32))

@@ -194,8 +194,8 @@ class pert_infer_scRT():
         self.init_method = init_method
         self.dirichlet_mode = dirichlet_mode
         self.n_jobs = n_jobs
-        # threads of the tau initialiser's exact host path (no worker processes): the affinity
-        # cores (at most 16) unless n_jobs > 1 names a count
+        # threads of the tau initialiser's exact host path (no worker processes): one
+        # (tau_init.default_threads) unless n_jobs > 1 names a count
         self.tau_threads = n_jobs if n_jobs > 1 else default_threads()
         self.tau_init_method = tau_init_method
         self.log_steps = log_steps

@@ -769,8 +769,12 @@ def exact_fractions(norm_cols: np.ndarray, labels=None, n_threads: int = 1, chun
 
 
 def default_threads() -> int:
-    """Threads of the exact host path: the affinity cores, at most 16."""
-    return max(1, min(16, len(os.sched_getaffinity(0))))
+    """Threads of the exact host path: one.  Its per-cell work is short numpy calls that hold
+    the GIL, so more threads do not go faster (C4's 1,831 flagged cells on the GPU box: 0.56 s
+    on 1 thread, 0.52-0.61 s on 2-16, profiles/r03za_exact_threads.log) and, inside a fit,
+    take the GIL from the thread queueing the device's steps (step 1 ran at 0.94 instead of
+    0.4 ms/step while 16 of them ran)."""
+    return 1
 
 
 def cn_normalise(reads: np.ndarray, cn_states: np.ndarray) -> np.ndarray:

@@ -807,9 +807,7 @@ def _consensus_blocks(cn: pd.DataFrame, col_name: str, clone_col: str, cn_state_
         lo, hi = int(st.min()), int(st.max())
         if lo < 0 or hi >= 4096:
             return None
-        sti = st.astype(np.int64)
-        cnt = np.bincount((np.arange(B, dtype=np.int64)[:, None] * (hi + 1) + sti).reshape(-1),
-                          minlength=B * (hi + 1)).reshape(B, hi + 1)
+        cnt = _row_state_counts(st, hi + 1)
         pl = cnt.argmax(axis=1)                          # modal state, ties to the smallest
         pu = np.unique(pl)
         pc = np.searchsorted(pu, pl)
@@ -821,6 +819,24 @@ def _consensus_blocks(cn: pd.DataFrame, col_name: str, clone_col: str, cn_state_
         if rows.size:
             med[:, c] = _column_median(vals, rows)
     return med, ku
+
+
+def _row_state_counts(st: np.ndarray, n_vals: int) -> np.ndarray:
+    """(B, n_vals) counts of each state in each row of the integer-valued (B, L) ``st``
+    (values in [0, n_vals)): one bincount per tile of rows, tiles on a few threads."""
+    from concurrent.futures import ThreadPoolExecutor
+    B = st.shape[0]
+    out = np.empty((B, n_vals), np.int64)
+    T = 256
+
+    def tile(b0):
+        s = st[b0:b0 + T].astype(np.int64)
+        n = s.shape[0]
+        out[b0:b0 + n] = np.bincount((np.arange(n, dtype=np.int64)[:, None] * n_vals + s).reshape(-1),
+                                     minlength=n * n_vals).reshape(n, n_vals)
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        list(ex.map(tile, range(0, B, T)))
+    return out
 
 
 def _column_median(vals: np.ndarray, rows: np.ndarray) -> np.ndarray:

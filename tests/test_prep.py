@@ -305,3 +305,13 @@ def test_transpose_cast_equals_numpy(shape):
         np.testing.assert_array_equal(got, np.ascontiguousarray(a.T).astype(dt))
     v = a[:, 1:]
     np.testing.assert_array_equal(prep.transpose_cast(v, np.int64), v.T.astype(np.int64))
+
+
+def test_row_state_counts_equals_bincount():
+    """prep._row_state_counts (threaded row tiles) counts each row's states like one bincount."""
+    rng = np.random.default_rng(8)
+    for B, L, V in [(1, 5, 3), (300, 41, 7), (257, 3, 13)]:
+        st = rng.integers(0, V, (B, L))
+        want = np.stack([np.bincount(r, minlength=V) for r in st])
+        np.testing.assert_array_equal(prep._row_state_counts(st, V), want)
+        np.testing.assert_array_equal(prep._row_state_counts(st.astype(np.float64), V), want)

@@ -208,6 +208,23 @@ int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream);
 int pert_adam(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
               hipStream_t stream);
 
+/* n whole SVI steps of a single-rank fit queued in one call (no all-reduce between the
+ * reductions and Adam, so one rank only): for i < n the step of loop iteration iter0 + i
+ * (st->step, the device loop's record index) with Adam hyper-parameters hp and
+ * hp->step_size = step_size[i], hp->inv_bc2_sqrt = inv_bc2_sqrt[i] (host arrays the caller
+ * computes for Adam steps t as torch.optim.Adam does: lr / (1 - beta1^t), 1 / sqrt(1 - beta2^t)).
+ * Each step is pert_enum_step(update_shared = 1) when one_launch (steps 2/3, variant 3), else
+ * pert_enum_pass(PERT_MODE_STEP) or pert_obs_pass, then pert_finalize and pert_adam.  With the
+ * device loop armed (loop_ctl), the steps after the stopping one are no-ops.  pass_events
+ * (NULL, or 2n caller-created events): events[2i] / events[2i+1] are recorded on the stream
+ * around step i's pass launch (the one launch of a one_launch step), for timing.  The call
+ * only queues launches (a few microseconds each), so a binding may release its interpreter
+ * lock around it.  Replaces n iterations of the svi.step loop of pert_model.py:742-758 /
+ * :800-816 / :867-883 (the loss record and stopping rule stay on the device). */
+int pert_svi_steps(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
+                   const float* step_size, const float* inv_bc2_sqrt, int32_t iter0, int32_t n,
+                   int32_t one_launch, hipEvent_t* pass_events, hipStream_t stream);
+
 /* Diagnostic (bench.py): the HBM streams of pert_enum_pass(PERT_MODE_STEP) -- x, eta code,
  * z/m/v read and written back unchanged, same grid and tile length -- with no arithmetic.
  * Its duration is the access pattern's HBM ceiling on the running device; the state is

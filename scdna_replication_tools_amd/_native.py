@@ -27,7 +27,8 @@ BLOCK = 256
 EXPORTED_SYMBOLS = (
     "pert_make_layout", "pert_workspace_sizes", "pert_auto_bins_per_tile", "pert_enum_pass", "pert_obs_pass",
     "pert_finalize", "pert_adam", "pert_enum_step", "pert_adam_shared", "pert_stream_ceiling", "pert_selftest_nb_lgdiff_host",
-    "pert_selftest_nb_lgdiff_device", "pert_selftest_enum_cellbin_host", "pert_tau_binarize", "pert_version",
+    "pert_selftest_nb_lgdiff_device", "pert_selftest_enum_cellbin_host", "pert_tau_binarize", "pert_svi_steps",
+    "pert_version",
 )
 
 
@@ -81,6 +82,7 @@ class PertAdamHparams(ctypes.Structure):
 
 
 _lib = None
+_lib_nogil = None
 
 
 def lib():
@@ -92,6 +94,17 @@ def lib():
         check_provenance(handle)
         _lib = handle
     return _lib
+
+
+def lib_nogil():
+    """The same library bound through ``ctypes.CDLL``: its calls release the interpreter lock.
+    For entry points that queue many launches at once (``pert_svi_steps``) or wait on the
+    device, so another thread of the fit runs Python meanwhile."""
+    global _lib_nogil
+    if _lib_nogil is None:
+        lib()                                   # presence, symbols and provenance checked once
+        _lib_nogil = load(LIB_PATH, gil=False)
+    return _lib_nogil
 
 
 def library_source_hash(handle) -> str:
@@ -111,9 +124,9 @@ def check_provenance(handle):
             "`python -m scdna_replication_tools_amd.build`)".format(LIB_PATH, got or "<unknown>", want))
 
 
-def load(path: str):
+def load(path: str, gil: bool = True):
     """Load and type one build of the C ABI (``lib()`` is the product one; A/B tools load
-    a second build beside it)."""
+    a second build beside it).  ``gil=False``: bound through CDLL (calls release the GIL)."""
     # torch first: its bundled libamdhip64 (soname libamdhip64.so.7) must be the one HIP
     # runtime of the process, so our kernels and torch's allocations share a context.
     import torch  # noqa: F401
@@ -126,7 +139,7 @@ def load(path: str):
         # no synchronisation), and a thread that drops the GIL around each launch waits for it
         # again behind whatever Python work another thread of the fit is doing (up to the
         # interpreter's switch interval per call), which starves the device of queued steps.
-        handle = ctypes.PyDLL(path)
+        handle = ctypes.PyDLL(path) if gil else ctypes.CDLL(path)
     except OSError as e:  # pragma: no cover
         raise NativeLibraryError("failed to load {}: {}".format(path, e))
     missing = [s for s in EXPORTED_SYMBOLS if not hasattr(handle, s)]
@@ -148,6 +161,8 @@ def load(path: str):
     handle.pert_adam_shared.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams),
                                         c_void_p]
     handle.pert_stream_ceiling.argtypes = [POINTER(PertProblem), POINTER(PertState), c_void_p]
+    handle.pert_svi_steps.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams), fp, fp,
+                                      i32, i32, i32, c_void_p, c_void_p]
     handle.pert_selftest_nb_lgdiff_host.argtypes = [i64, fp, fp, fp, fp]
     handle.pert_selftest_nb_lgdiff_device.argtypes = [i64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     handle.pert_selftest_enum_cellbin_host.argtypes = [i32, i64, fp, fp, fp, fp, c_float, fp, fp, fp, fp,

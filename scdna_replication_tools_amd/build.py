@@ -134,21 +134,32 @@ def host_source_hash() -> str:
     return h.hexdigest()[:HASH_LEN]
 
 
+def host_embedded_hash(path: str = HOST_OUT):
+    """The source hash baked into libpert_host.so (``pert_host_version()``, read from its bytes)."""
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as fh:
+        m = re.search(rb"pert_host src=([0-9a-f]{%d})" % HASH_LEN, fh.read())
+    return m.group(1).decode() if m else None
+
+
 def build_host(force: bool = False) -> str:
-    """libpert_host.so (gcc): the CPU helpers of tau_init's exact path.  Rebuilt when the
-    hash of its sources (kept in a stamp file beside it) changes."""
-    stamp = HOST_OUT + ".src"
+    """libpert_host.so (gcc): the CPU helpers of tau_init's exact path.  The hash of its
+    sources is compiled into it (``pert_host_version()``); it is rebuilt when that differs
+    from the tree's, and tau_init refuses a library whose hash does not match."""
     want = host_source_hash()
-    if not force and os.path.exists(HOST_OUT) and os.path.exists(stamp) and open(stamp).read().strip() == want:
+    if not force and host_embedded_hash() == want:
         return HOST_OUT
-    cmd = [os.environ.get("CC", "gcc"), *HOST_FLAGS, *HOST_SOURCES, "-o", HOST_OUT + ".tmp"]
+    cmd = [os.environ.get("CC", "gcc"), *HOST_FLAGS, '-DPERT_HOST_SRC="{}"'.format(want), *HOST_SOURCES,
+           "-o", HOST_OUT + ".tmp"]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         sys.stderr.write(res.stdout + res.stderr)
         raise RuntimeError("gcc failed building {}".format(HOST_OUT))
     os.replace(HOST_OUT + ".tmp", HOST_OUT)
-    with open(stamp, "w") as fh:
-        fh.write(want)
+    stale = HOST_OUT + ".src"                     # the stamp file of earlier builds
+    if os.path.exists(stale):
+        os.remove(stale)
     return HOST_OUT
 
 

@@ -52,6 +52,13 @@ static float pairwise(const float* a, int64_t n) {
 
 float pert_host_pairwise_sum(const float* a, int64_t n) { return pairwise(a, n); }
 
+/* "pert_host src=<hash>": the hash of the sources and flags this binary was built from
+ * (build.py build_host passes it in); tau_init refuses a library whose hash differs. */
+#ifndef PERT_HOST_SRC
+#define PERT_HOST_SRC "unknown"
+#endif
+const char* pert_host_version(void) { return "pert_host src=" PERT_HOST_SRC; }
+
 /* One M step and lower bound for the cells ``rows`` (m of them) of an EM chunk.
  *   resp_u  (m, U, 2)  responsibilities of each cell's distinct values (E step output)
  *   lpn_u   (m, U)     their log p(x) (NULL: no lower bound, the initial M step)

@@ -1533,13 +1533,15 @@ __global__ void __launch_bounds__(kFinBlock) finalize_kernel(pert_problem pr, pe
 //   losses.append(loss)
 //   if i >= min_iter: stop if |max(losses[-10:-1]) - min(losses[-10:-1])| / |losses[0] - losses[-1]| < rel_tol
 //   if isnan(loss): stop
-// in fp64 on the same values the host would see, so the stopping iteration is the host's.
+// The loss is accumulated in fp64 and recorded as the fp32 value the reference appends
+// (``float(loss)`` of its fp32 ELBO tensor); the rule itself runs in fp64 on those values,
+// as Python's floats do, so the stopping iteration is the host's.
 // (The reference raises on an empty window (min_iter = 0 at i = 0) or a zero denominator;
 // here those iterations simply do not stop.)
 __device__ void loop_record(const pert_state& st) {
   const int t = st.step;
-  const double loss = st.grad_shared[st.lay.n_shared] - st.loss_const -
-                      (st.loss_offset != nullptr ? st.loss_offset[t] : 0.0);
+  const double loss = (double)(float)(st.grad_shared[st.lay.n_shared] - st.loss_const -
+                                      (st.loss_offset != nullptr ? st.loss_offset[t] : 0.0));
   double* rec = st.loop_rec;
   int reason = 0;
   if (t >= st.min_iter) {
@@ -2309,6 +2311,37 @@ int pert_adam(const pert_problem* prob, pert_state* st, const pert_adam_hparams*
   const int n = st->lay.n_params;
   hipLaunchKernelGGL(adam_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, *prob, *st, *hp, n);
   return hip_status(hipGetLastError());
+}
+
+int pert_svi_steps(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp, const float* step_size,
+                   const float* inv_bc2_sqrt, int32_t iter0, int32_t n, int32_t one_launch, hipEvent_t* pass_events,
+                   hipStream_t stream) {
+  if (!problem_ok(prob) || !st || !hp || !step_size || !inv_bc2_sqrt || n < 0 || iter0 < 0) return PERT_E_ARG;
+  const bool enumerated = prob->kind == PERT_KIND_STEP2 || prob->kind == PERT_KIND_STEP3;
+  if (one_launch && (!enumerated || st->variant != 3)) return PERT_E_ARG;
+  pert_state s = *st;
+  pert_adam_hparams h = *hp;
+  int rc = PERT_OK;
+  auto mark = [&](int32_t i, int which) {
+    if (pass_events && rc == PERT_OK) rc = hip_status(hipEventRecord(pass_events[2 * i + which], stream));
+  };
+  for (int32_t i = 0; i < n && rc == PERT_OK; ++i) {
+    s.step = iter0 + i;                        // the loop record's iteration index
+    h.step_size = step_size[i];
+    h.inv_bc2_sqrt = inv_bc2_sqrt[i];
+    mark(i, 0);
+    if (one_launch) {
+      if (rc == PERT_OK) rc = pert_enum_step(prob, &s, &h, 1, stream);
+      mark(i, 1);
+      continue;
+    }
+    if (rc == PERT_OK)
+      rc = enumerated ? pert_enum_pass(prob, &s, &h, PERT_MODE_STEP, stream) : pert_obs_pass(prob, &s, stream);
+    mark(i, 1);
+    if (rc == PERT_OK) rc = pert_finalize(prob, &s, stream);
+    if (rc == PERT_OK) rc = pert_adam(prob, &s, &h, stream);
+  }
+  return rc;
 }
 
 int pert_stream_ceiling(const pert_problem* prob, pert_state* st, hipStream_t stream) {

@@ -268,6 +268,9 @@ class PertShard:
                  dirichlet_mode: str = "torch32", bins_per_tile: int = 0, variant: int = 3, fused: bool = False,
                  paired: bool = False, lib=None):
         self.lib = nat.lib() if lib is None else lib        # another build of the ABI (A/B tools)
+        # the chunked SVI loop's handle: the product library through CDLL (the call releases the
+        # GIL while it queues its launches); an A/B build keeps its own handle
+        self._lib_chunk = nat.lib_nogil() if lib is None else (lib if hasattr(lib, "pert_svi_steps") else None)
         self.kind = int(kind)
         self.variant = int(variant)
         # one launch per SVI step (pert_enum_step): the three-wave pass of steps 2/3
@@ -671,26 +674,49 @@ class PertShard:
         st = self._state
         st.loop_ctl, st.loop_rec, st.loss_offset = _ptr(ctl), _ptr(rec), _ptr(offs)
         st.loss_const, st.rel_tol, st.min_iter = float(self.const_total), float(rel_tol), int(min_iter)
+        # one rank: a chunk of iterations is queued by ONE C call (pert_svi_steps) that releases
+        # the GIL, instead of ~3 GIL-holding calls per iteration; per-pass timing events, when
+        # asked for (pass_events), are recorded by that call around each pass
+        chunked = self.allreduce is None and self._lib_chunk is not None
+        b1, b2 = self.betas
         launched = 0
         pending = []
         try:
-            for i in range(n):
-                st.step = i
-                self._launch_step(t0 + i + 1)
-                launched += 1
-                if (i + 1) % chunk == 0 or i == n - 1:
-                    j0 = (i // chunk) * chunk
-                    host[j0:i + 1].copy_(rec[j0:i + 1], non_blocking=True)
-                    ev = torch.cuda.Event()
-                    ev.record()
-                    pending.append((j0, i + 1, ev))
-                    stop_seen = False
-                    while len(pending) > depth:
-                        a, b, e = pending.pop(0)
-                        e.synchronize()
-                        stop_seen = stop_seen or bool((host[a:b, 1] >= 0).any())
-                    if stop_seen:
-                        break
+            for j0 in range(0, n, chunk):
+                j1 = min(n, j0 + chunk)
+                if chunked:
+                    ts = range(t0 + j0 + 1, t0 + j1 + 1)
+                    ss = np.array([self.lr / (1.0 - b1 ** t) for t in ts], dtype=F32)     # as _set_hparams
+                    ib = np.array([1.0 / math.sqrt(1.0 - b2 ** t) for t in ts], dtype=F32)
+                    evp = None
+                    if self.pass_events is not None:
+                        evs = [torch.cuda.Event(enable_timing=True) for _ in range(2 * (j1 - j0))]
+                        for e in evs:
+                            e.record()                     # creates the HIP event behind it
+                        evp = (ctypes.c_void_p * len(evs))(*[e.cuda_event for e in evs])
+                        self.pass_events.extend(zip(evs[0::2], evs[1::2]))
+                    with self._dev():
+                        nat.check(self._lib_chunk.pert_svi_steps(
+                            ctypes.byref(self._prob), ctypes.byref(st), ctypes.byref(self._hp),
+                            ss.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                            ib.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), j0, j1 - j0, 1 if self.fused else 0,
+                            evp, self._stream()), "pert_svi_steps")
+                else:
+                    for i in range(j0, j1):
+                        st.step = i
+                        self._launch_step(t0 + i + 1)
+                launched = j1
+                host[j0:j1].copy_(rec[j0:j1], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                pending.append((j0, j1, ev))
+                stop_seen = False
+                while len(pending) > depth:
+                    a, b, e = pending.pop(0)
+                    e.synchronize()
+                    stop_seen = stop_seen or bool((host[a:b, 1] >= 0).any())
+                if stop_seen:
+                    break
             c = ctl.cpu()                      # waits for every queued launch and copy
         finally:
             st.loop_ctl = st.loop_rec = st.loss_offset = None
@@ -704,11 +730,12 @@ class PertShard:
         return losses, (reason if stop_at >= 0 else 0)
 
     def device_loss(self) -> float:
-        """Loss of the last step: -(ELBO) with the host constants (pert_model.py:743 return value)."""
+        """Loss of the last step: -(ELBO) with the host constants (pert_model.py:743 return value),
+        accumulated in fp64 and returned as the fp32 value ``float(loss)`` gives the reference."""
         loss = float(self.grad_shared[self.lay.n_shared].item()) - self.const_total
         if self.pi_block is not None:
             loss -= self.L * self.n_cells_total * self._pi_lp
-        return loss
+        return float(np.float32(loss))
 
     def step(self) -> float:
         self.step_async()

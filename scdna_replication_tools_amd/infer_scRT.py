@@ -34,8 +34,10 @@ def assign_s_to_clones(s_phase_cells: pd.DataFrame, clone_df: pd.DataFrame, col_
     if lay is not None:
         B, L, bp, q, ch0 = lay
         cells = np.ascontiguousarray(s[cell_col].to_numpy())[::L][bp]
+        # float64 like the general pivot and the reference's pearsonr: the block pivot keeps an
+        # integer column in float32, where the centring and norms would round differently
         piv = prep.Pivot(cells, np.array(prep.CHR_ORDER, dtype=object)[ch0[q]], s[start_col].to_numpy()[:L][q],
-                         prep._block_pivot(s[col_name].to_numpy(), B, L, bp, q))
+                         prep._block_pivot(s[col_name].to_numpy(), B, L, bp, q).astype(np.float64, copy=False))
         pos = np.empty(B, np.int64)
         pos[bp] = np.arange(B)                     # block (table order) -> sorted cell index
         row_cell = np.repeat(pos, L)

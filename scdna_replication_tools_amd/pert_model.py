@@ -32,7 +32,6 @@ from __future__ import annotations
 import contextlib
 import logging
 import os
-import sys
 import time
 from typing import List, Optional
 
@@ -427,12 +426,10 @@ class pert_infer_scRT():
         # tau initialisation while step 1 fits, then (during step 2) the step-3 prior and tau
         # initialisation -- device parts on a side stream
         from concurrent.futures import ThreadPoolExecutor
+        # (the fit thread queues chunks of iterations by GIL-releasing C calls, 64 iterations
+        # ahead of the device -- more than the interpreter's 5 ms switch interval lasts -- so the
+        # helper's Python work does not starve the device, PertShard.run_svi)
         helper = ThreadPoolExecutor(max_workers=1, thread_name_prefix="pert-prep")
-        # the fit thread queues launches ahead of the device and gives up the GIL only while it
-        # waits on the device; a helper thread running Python would otherwise keep it for the
-        # interpreter's default 5 ms switch interval, longer than the queue of steps lasts
-        switch = sys.getswitchinterval()
-        sys.setswitchinterval(min(switch, 5e-4))
 
         def on_device(fn, *a):
             # the HIP runtime's current device is per thread: the helper uses the fit's device
@@ -557,7 +554,6 @@ class pert_infer_scRT():
         finally:
             # also when a fit or a helper task raised: no helper work outlives the call
             helper.shutdown(wait=True, cancel_futures=True)
-            sys.setswitchinterval(switch)
         self.timings["total"] = time.perf_counter() - t_all
         return cn_s_out, supp_s_out_df, cn_g1_out, supp_g1_out_df
 

@@ -19,8 +19,6 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import List, Optional
 
-import os
-
 import numpy as np
 import pandas as pd
 
@@ -1177,21 +1175,20 @@ def manhattan_binarization(X: np.ndarray, MEAN_GAP_THRESH=0.7, EARLY_S_SKEW_THRE
 
 
 def guess_times(reads: np.ndarray, cn_states: np.ndarray, upsilon: float = 6, n_jobs: int = 1):
-    """pert_model.py:426-457: t_init, t_alpha_prior, t_beta_prior per cell."""
+    """pert_model.py:426-457: t_init, t_alpha_prior, t_beta_prior per cell.
+
+    The cells are fitted one after another, as the reference loops over them, whatever
+    ``n_jobs`` says (kept for the signature): GaussianMixture's k-means runs inside
+    sklearn's per-call threadpoolctl limit, and that limit, entered from several threads of
+    one process at once, races OpenBLAS's thread-count setter against the other threads'
+    BLAS calls (a 10k-cell run deadlocked on it)."""
     import torch
+    del n_jobs
     x = torch.as_tensor(reads, dtype=torch.float32)
     st = torch.as_tensor(cn_states, dtype=torch.float32)
     half = (torch.ones(x.shape) * 0.5).type(torch.float32)
     norm = (x / torch.where(st > 0.0, st, half)).numpy()
-    cols = [norm[:, i].reshape(-1, 1) for i in range(norm.shape[1])]
-    if n_jobs != 1:
-        # threads of this process (no worker processes); -1: the affinity cores, at most 16
-        from concurrent.futures import ThreadPoolExecutor
-        nt = n_jobs if n_jobs > 0 else max(1, min(16, len(os.sched_getaffinity(0))))
-        with ThreadPoolExecutor(max_workers=nt) as ex:
-            fr = list(ex.map(manhattan_binarization, cols))
-    else:
-        fr = [manhattan_binarization(c) for c in cols]
+    fr = [manhattan_binarization(norm[:, i].reshape(-1, 1)) for i in range(norm.shape[1])]
     t_init = np.array([f[1] for f in fr], dtype=np.float32)
     alpha = (t_init * upsilon).astype(np.float32)
     return t_init, alpha, (upsilon - alpha).astype(np.float32)

@@ -46,16 +46,47 @@ import torch
 # the per-cell reference path's modules, imported with this one (as pert_model.py:18-20
 # imports them): the exact host path calls them
 from scipy.stats import skew
-from sklearn.cluster._kmeans import _kmeans_single_lloyd, _tolerance
+from sklearn.cluster import KMeans
 
-# sklearn wraps its Lloyd in a threadpoolctl limit of 1 BLAS thread (utils/parallel.py
-# _threadpool_controller_decorator), which sets and restores OpenBLAS's thread count around
-# every call.  From the exact path's threads those calls race each other and the BLAS calls
-# of the other threads (openblas_set_num_threads during a BLAS call in flight), which
-# deadlocked a 10k-cell run; the unwrapped function is called instead.  Its BLAS work (gemm of
-# a 256-sample chunk by 2 one-feature centres) is below OpenBLAS's threading threshold, so it
-# runs on one thread either way and the labels are the same.
-_lloyd_unwrapped = getattr(_kmeans_single_lloyd, "__wrapped__", _kmeans_single_lloyd)
+
+def _private_lloyd():
+    """sklearn's own Lloyd iteration (cluster/_kmeans.py ``_kmeans_single_lloyd``), unwrapped,
+    or None when this sklearn does not have it with the signature used here.
+
+    It is a private function, so it is only taken after checking its parameters; otherwise
+    ``exact_kmeans_labels`` runs the public ``KMeans(...).fit`` call GaussianMixture itself
+    makes (same labels, ~1 ms more per cell).  sklearn wraps the function in a threadpoolctl
+    limit of 1 BLAS thread (utils/parallel.py _threadpool_controller_decorator) that sets and
+    restores OpenBLAS's thread count around every call; entered from several threads at once
+    those calls race each other and the other threads' BLAS calls (a 10k-cell run
+    deadlocked), so the unwrapped function is called.  Its BLAS work (gemm of a 256-sample
+    chunk by 2 one-feature centres) is below OpenBLAS's threading threshold: one thread
+    either way, same labels."""
+    import inspect
+    try:
+        from sklearn.cluster._kmeans import _kmeans_single_lloyd as f
+    except ImportError:
+        return None
+    f = getattr(f, "__wrapped__", f)
+    try:
+        names = list(inspect.signature(f).parameters)
+    except (TypeError, ValueError):
+        return None
+    want = ["X", "sample_weight", "centers_init", "max_iter", "verbose", "tol", "n_threads"]
+    return f if names[:len(want)] == want else None
+
+
+_lloyd_unwrapped = _private_lloyd()
+# the public fallback enters threadpoolctl on every call: one caller at a time
+_KMEANS_LOCK = threading.Lock()
+
+
+def _tolerance(X: np.ndarray, tol: float) -> float:
+    """sklearn cluster/_kmeans.py ``_tolerance`` for dense X: mean of the per-feature
+    variances times tol."""
+    if tol == 0:
+        return 0
+    return np.mean(np.var(X, axis=0)) * tol
 
 MEAN_GAP_THRESH = 0.7
 EARLY_S_SKEW_THRESH = 0.2
@@ -462,8 +493,11 @@ def exact_kmeans_labels(x: np.ndarray) -> np.ndarray:
     the uncentred data, centring by the fp32 mean, k-means++ (``_kmeans_plusplus`` restated
     with the same RandomState draws, distances and BLAS products), then sklearn's own Lloyd
     (``_kmeans_single_lloyd``, on one OpenMP thread: the reference's thread count only
-    changes the last bits of the centre sums, never a label short of an exact tie)."""
+    changes the last bits of the centre sums, never a label short of an exact tie).  Without
+    that function (``_private_lloyd``) the public call itself runs."""
     X = np.array(x, dtype=F32, order="C").reshape(-1, 1)
+    if _lloyd_unwrapped is None:
+        return public_kmeans_labels(X)
     n = X.shape[0]
     tol = _tolerance(X, 1e-4)
     rs = np.random.RandomState(0)
@@ -481,6 +515,16 @@ def exact_kmeans_labels(x: np.ndarray) -> np.ndarray:
     centers[1] = X[cand[np.argmin(dc @ sw.reshape(-1, 1))]]
     labels, _, _, _ = _lloyd_unwrapped(X, sw, centers, max_iter=300, verbose=False, tol=tol, n_threads=1)
     return labels.astype(np.int8)
+
+
+def public_kmeans_labels(x: np.ndarray) -> np.ndarray:
+    """GaussianMixture's k-means initialisation through sklearn's public API, the call of
+    mixture/_base.py ``_initialize_parameters``: ``KMeans(n_clusters=2, n_init=1,
+    random_state=<RandomState(0)>).fit(X).labels_`` (one caller at a time)."""
+    X = np.array(x, dtype=F32, order="C").reshape(-1, 1)
+    with _KMEANS_LOCK:
+        km = KMeans(n_clusters=2, n_init=1, random_state=np.random.RandomState(0)).fit(X)
+    return km.labels_.astype(np.int8)
 
 
 def _lse2(a: np.ndarray) -> np.ndarray:
@@ -529,6 +573,11 @@ class _HostHelper:
         path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpert_host.so")
         blas = _numpy_blas()
         if blas is None or not os.path.exists(path):
+            return None
+        from . import build as _build
+        # a library built from other sources (an ABI or arithmetic change) is not loaded:
+        # the numpy restatement runs instead
+        if _build.host_embedded_hash(path) != _build.host_source_hash():
             return None
         try:
             lib = ctypes.CDLL(path)                       # CDLL: the calls release the GIL

@@ -167,3 +167,24 @@ def test_assign_per_cell_block_table_matches_reference_loop(ids):
     general = assign_s_to_clones(s.sample(frac=1.0, random_state=3).reset_index(drop=True), prof.copy(),
                                  col_name="copy")
     assert got["clone_id"].dtype == general["clone_id"].dtype
+
+
+def test_assign_block_table_integer_column_in_float64():
+    """An integer read-count column (the default col_name='reads') on the per-cell-block
+    path: the correlations run in float64 like the general path and the reference, so
+    near-tied clones are assigned alike."""
+    from scdna_replication_tools_amd import prep
+    rng = np.random.default_rng(23)
+    ids = ["A", "B", "C"]
+    loci = _loci()
+    prof = _clones(ids, loci, rng)
+    s = _cells(prof, loci, 30, rng, ids, inf_nan=False)
+    s["reads"] = np.round(s["copy"].to_numpy() * 1e5).astype(np.int64)    # large counts: fp32 would round
+    s = s.sort_values(["cell_id", "chr", "start"], kind="stable").reset_index(drop=True)
+    s["cell_id"] = s["cell_id"].map({c: c for c in s["cell_id"].unique()})   # one str object per cell
+    assert prep._block_layout(s, "cell_id", "chr", "start", "reads") is not None
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        ref = _ref_assign(s.copy(), prof.copy(), col_name="reads")
+        got = assign_s_to_clones(s.copy(), prof.copy(), col_name="reads")
+    assert (got["clone_id"].to_numpy() == ref["clone_id"].to_numpy()).all()

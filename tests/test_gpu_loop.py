@@ -88,6 +88,30 @@ def test_device_loop_stops_on_nan(variant, fused):
     assert sh.t == 1
 
 
+@pytest.mark.parametrize("variant,fused", VARIANTS)
+@pytest.mark.parametrize("kind", ["step2", "step1p"])
+def test_chunked_loop_equals_per_step_launches(kind, variant, fused):
+    """run_svi's one-call chunks (pert_svi_steps through the GIL-releasing handle), with and
+    without the per-pass timing events, equal the per-step launch sequence bit for bit."""
+    if fused and kind.startswith("step1"):
+        pytest.skip("step 1 has no one-launch form")
+    prob, kw, z = make_problem(kind, seed=5)
+    per_step = _shard(kind, kw, z, variant=variant, fused=fused)
+    per_step._lib_chunk = None                      # the per-iteration launches of _launch_step
+    la, ra = per_step.run_svi(19, 10 ** 9, 0.0)
+    b = _shard(kind, kw, z, variant=variant, fused=fused)
+    lb, rb = b.run_svi(19, 10 ** 9, 0.0)
+    c = _shard(kind, kw, z, variant=variant, fused=fused)
+    c.pass_events = []
+    lc, rc = c.run_svi(19, 10 ** 9, 0.0)
+    assert la == lb == lc and ra == rb == rc == 0
+    assert len(c.pass_events) == 19 and all(e0.elapsed_time(e1) > 0 for e0, e1 in c.pass_events)
+    sa, sb, sc = _state(per_step), _state(b), _state(c)
+    for k in sa:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+        np.testing.assert_array_equal(sa[k], sc[k], err_msg=k)
+
+
 def test_device_loop_chunk_boundaries():
     """Stopping iterations on either side of a read-back chunk boundary."""
     prob, kw, z = make_problem("step2", seed=8)

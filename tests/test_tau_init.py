@@ -80,6 +80,30 @@ def test_exact_stages_match_sklearn_bit_for_bit(L, seed):
     np.testing.assert_array_equal(tau_init.exact_gmm_means(Xs, labs), ref_means)
 
 
+def test_private_lloyd_is_checked_and_public_fallback_equal(monkeypatch):
+    """The private sklearn Lloyd is only used after its signature check; without it the
+    exact path runs the public KMeans call GaussianMixture makes, with the same labels and
+    the same t_init for every cell."""
+    assert tau_init._lloyd_unwrapped is not None, "this sklearn's _kmeans_single_lloyd signature changed"
+    reads, states = _profiles(n_s=24, n_g=8, L=271, seed=17)
+    Xs = tau_init.standardize_rows(_norm(reads, states).T)
+    for n in range(Xs.shape[0]):
+        np.testing.assert_array_equal(tau_init.exact_kmeans_labels(Xs[n]), tau_init.public_kmeans_labels(Xs[n]))
+    monkeypatch.setattr(tau_init, "_lloyd_unwrapped", None)
+    fr = tau_init.exact_fractions(_norm(reads, states), None, n_threads=2, chunk=8).astype(np.float32)
+    np.testing.assert_array_equal(fr, prep.guess_times(reads, states, upsilon=6)[0])
+
+
+def test_sklearn_guess_times_ignores_n_jobs():
+    """prep.guess_times (tau_init_method='sklearn') fits the cells one after another for
+    any n_jobs (sklearn's threadpool limit is not safe from several threads)."""
+    reads, states = _profiles(n_s=10, n_g=4, L=271, seed=19)
+    t1 = prep.guess_times(reads, states, upsilon=6, n_jobs=1)
+    t4 = prep.guess_times(reads, states, upsilon=6, n_jobs=4)
+    for a, b in zip(t1, t4):
+        np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("L,seed", [(271, 6), (5451, 9)])
 def test_exact_path_alone_matches_reference_every_cell(L, seed):
     """Every cell through the exact host path (k-means on the host too), on 4 threads:

@@ -1,0 +1,111 @@
+"""Where does step 2's stopping iteration come from?  (test infrastructure, CPU only)
+
+Re-runs step 2 of the genome-length oracle chain (tests/golden/make_genome_chain_golden.py)
+alone, from the fixture's step-1 sites (lambda, beta_means) and t_init, in variants of the
+per-element arithmetic, and prints where pert_model.py:807-811's rule stops each one:
+
+  ref          the fp32 oracle as committed (torch autograd of torch.distributions, the
+               tensor algebra Pyro runs) -- must reproduce the fixture's trace and stop
+  logsoftmax   the Dirichlet term's xlogy(eta-1, pi) evaluated as (eta-1) * log_softmax(z):
+               the same value, but its gradient is cancellation-free (the product's form,
+               SURVEY.md Appendix C) instead of (eta-1)/pi pushed back through the softmax
+  detach_max   SoftmaxTransform with its max detached (mathematically the same gradient;
+               in fp32 the softmax backward's residue sum_k dL/dp_k p_k no longer lands on
+               the argmax logit)
+
+Run under ``ATEN_CPU_CAPABILITY=default|avx2|avx512`` for the reference's own fp32 arithmetic
+on CPUs with other vector units (torch CPU picks its exp / log / reduction kernels by ISA).
+
+    python tools/stop_probe.py ref [--threads 4] [--out file.npz]
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from oracle import pert_oracle as po  # noqa: E402
+from tests._chain import _t, _z0  # noqa: E402
+from tests._configs import genome_scrt, genome_tables  # noqa: E402
+from scdna_replication_tools_amd import prep  # noqa: E402
+from scdna_replication_tools_amd.init import init_params  # noqa: E402
+
+FIXTURE = os.path.join(ROOT, "tests", "golden", "genome_chain_oracle.npz")
+
+
+def _patch(variant):
+    if variant == "detach_max":
+        from torch.distributions.transforms import SoftmaxTransform
+
+        def _call(self, x):
+            probs = (x - x.max(-1, True)[0].detach()).exp()
+            return probs / probs.sum(-1, True)
+        SoftmaxTransform._call = _call
+    elif variant == "logsoftmax":
+        base = po.elbo
+
+        def elbo(prob, z, **kw):
+            c = po.constrain(prob.kind, z)
+            terms = po.model_terms(prob, c, **kw)
+            e = prob.etas
+            terms["expose_pi"] = ((e - 1.0) * torch.log_softmax(z["expose_pi"], -1)).sum() + (
+                torch.lgamma(e.sum(-1)) - torch.lgamma(e).sum(-1)).sum()
+            return sum(terms.values())
+        po.elbo = elbo
+        assert base is not po.elbo
+    elif variant != "ref":
+        raise SystemExit("unknown variant " + variant)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("variant")
+    ap.add_argument("--threads", type=int, default=4)
+    ap.add_argument("--max-iter", type=int, default=None)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    torch.set_num_threads(a.threads)
+    _patch(a.variant)
+    fx = dict(np.load(FIXTURE))
+    s, g, _ = genome_tables()
+    m = genome_scrt(s, g, device="cpu")._pert_model()
+    inp = m._prepare()
+    P, K, nl = m.P, m.K, m.L
+    profiles = prep.consensus_clone_profiles(m.cn_g1, m.cn_state_col, clone_col=m.clone_col, cell_col=m.cell_col,
+                                             chr_col=m.chr_col, start_col=m.start_col, cn_state_col=m.cn_state_col,
+                                             keys=inp.keys_g)
+    etas = m._build_etas(inp, profiles)
+    lam, bm, t_init = fx["lam"], fx["beta_means"], fx["t_init_s"]
+    dt = torch.float32
+    ploidy = etas.argmax_states().astype(np.float32).mean(0)
+    L, N = inp.reads_s.shape
+    init2 = init_params(2, inp.reads_s, inp.libs_s, nl, P, K, ploidy=ploidy, t_init=t_init, beta_means=bm,
+                        seed=m.seed, method=m.init_method)
+    prob = po.OracleProblem("step2", _t(inp.reads_s, dt), _t(inp.gc, dt), torch.as_tensor(inp.libs_s, dtype=torch.long),
+                            nl, P, K, etas=_t(etas.dense(), dt), lamb=_t(lam, dt), beta_means=_t(bm, dt),
+                            t_init=_t(t_init, dt))
+    t0 = time.perf_counter()
+
+    def cb(i, lval):
+        if i % 50 == 0:
+            ref = fx["losses_s"][i] if i < len(fx["losses_s"]) else float("nan")
+            print("it {} loss {:.1f} fixture {:.1f} {:.0f}s".format(i, lval, ref, time.perf_counter() - t0), flush=True)
+    r = po.fit(prob, _z0("step2", init2, L, N, P, dt), lr=m.learning_rate, max_iter=a.max_iter or m.max_iter,
+               min_iter=m.min_iter, rel_tol=m.rel_tol, callback=cb)
+    losses = np.asarray(r.losses)
+    n = min(len(losses), len(fx["losses_s"]))
+    dev = np.abs(losses[:n] - fx["losses_s"][:n])
+    cap = torch.backends.cpu.get_cpu_capability()
+    print("variant {} capability {} stop {} (fixture {}) first-iteration dev {:.1f} max dev {:.1f} at {}".format(
+        a.variant, cap, len(losses), len(fx["losses_s"]), dev[0], dev.max(), int(dev.argmax())), flush=True)
+    if a.out:
+        np.savez_compressed(a.out, losses=losses, variant=a.variant, capability=cap)
+
+
+if __name__ == "__main__":
+    main()

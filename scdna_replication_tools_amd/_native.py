@@ -28,7 +28,7 @@ EXPORTED_SYMBOLS = (
     "pert_make_layout", "pert_workspace_sizes", "pert_auto_bins_per_tile", "pert_enum_pass", "pert_obs_pass",
     "pert_finalize", "pert_adam", "pert_enum_step", "pert_adam_shared", "pert_stream_ceiling", "pert_selftest_nb_lgdiff_host",
     "pert_selftest_nb_lgdiff_device", "pert_selftest_enum_cellbin_host", "pert_tau_binarize", "pert_svi_steps",
-    "pert_version",
+    "pert_svi_run", "pert_version",
 )
 
 
@@ -98,8 +98,8 @@ def lib():
 
 def lib_nogil():
     """The same library bound through ``ctypes.CDLL``: its calls release the interpreter lock.
-    For entry points that queue many launches at once (``pert_svi_steps``) or wait on the
-    device, so another thread of the fit runs Python meanwhile."""
+    For entry points that queue many launches at once (``pert_svi_steps``) or run a whole fit
+    (``pert_svi_run``), so another thread of the fit runs Python meanwhile."""
     global _lib_nogil
     if _lib_nogil is None:
         lib()                                   # presence, symbols and provenance checked once
@@ -163,6 +163,8 @@ def load(path: str, gil: bool = True):
     handle.pert_stream_ceiling.argtypes = [POINTER(PertProblem), POINTER(PertState), c_void_p]
     handle.pert_svi_steps.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams), fp, fp,
                                       i32, i32, i32, c_void_p, c_void_p]
+    handle.pert_svi_run.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams), fp, fp,
+                                    i32, i32, i32, i32, c_void_p, POINTER(i32), c_void_p]
     handle.pert_selftest_nb_lgdiff_host.argtypes = [i64, fp, fp, fp, fp]
     handle.pert_selftest_nb_lgdiff_device.argtypes = [i64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     handle.pert_selftest_enum_cellbin_host.argtypes = [i32, i64, fp, fp, fp, fp, c_float, fp, fp, fp, fp,

@@ -2344,6 +2344,47 @@ int pert_svi_steps(const pert_problem* prob, pert_state* st, const pert_adam_hpa
   return rc;
 }
 
+int pert_svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp, const float* step_size,
+                 const float* inv_bc2_sqrt, int32_t n_iter, int32_t chunk, int32_t depth, int32_t one_launch,
+                 double* host_rec, int32_t* n_launched, hipStream_t stream) {
+  if (!st || !st->loop_ctl || !st->loop_rec || !host_rec || !n_launched || n_iter < 0 || chunk < 1 || depth < 1)
+    return PERT_E_ARG;
+  *n_launched = 0;
+  if (n_iter == 0) return PERT_OK;
+  const int n_chunks = (n_iter + chunk - 1) / chunk;
+  const int ring = depth + 1;
+  hipEvent_t ev[64];
+  if (ring > 64) return PERT_E_ARG;
+  int rc = PERT_OK, made = 0;
+  for (; made < ring && rc == PERT_OK; ++made)
+    rc = hip_status(hipEventCreateWithFlags(&ev[made], hipEventDisableTiming | hipEventBlockingSync));
+  int waited = 0;                              // chunks whose records have been looked at
+  bool stop_seen = false;
+  int c = 0;
+  // a chunk's records are at host_rec[2 j] (loss) and host_rec[2 j + 1] (>= 0: stopped at j)
+  auto look = [&](int k) {
+    rc = rc == PERT_OK ? hip_status(hipEventSynchronize(ev[k % ring])) : rc;
+    const int j1 = (k + 1) * chunk < n_iter ? (k + 1) * chunk : n_iter;
+    for (int j = k * chunk; j < j1 && rc == PERT_OK; ++j)
+      if (host_rec[2 * j + 1] >= 0.0) stop_seen = true;
+  };
+  for (; c < n_chunks && rc == PERT_OK && !stop_seen; ++c) {
+    if (c - waited >= ring - 1) look(waited++);          // the ring's oldest chunk is done
+    if (stop_seen || rc != PERT_OK) break;
+    const int j0 = c * chunk, n = (j0 + chunk < n_iter ? j0 + chunk : n_iter) - j0;
+    rc = pert_svi_steps(prob, st, hp, step_size + j0, inv_bc2_sqrt + j0, j0, n, one_launch, nullptr, stream);
+    if (rc == PERT_OK)
+      rc = hip_status(hipMemcpyAsync(host_rec + 2 * j0, st->loop_rec + 2 * j0, sizeof(double) * 2 * n,
+                                     hipMemcpyDeviceToHost, stream));
+    if (rc == PERT_OK) rc = hip_status(hipEventRecord(ev[c % ring], stream));
+    if (rc == PERT_OK) *n_launched = j0 + n;
+  }
+  const hipError_t e = hipStreamSynchronize(stream);     // every queued launch and copy
+  if (rc == PERT_OK) rc = hip_status(e);
+  for (int k = 0; k < made; ++k) hipEventDestroy(ev[k]);
+  return rc;
+}
+
 int pert_stream_ceiling(const pert_problem* prob, pert_state* st, hipStream_t stream) {
   if (!problem_ok(prob) || !st || !st->z_pi || !st->m_pi || !st->v_pi || !prob->eta_code) return PERT_E_ARG;
   if (prob->kind != PERT_KIND_STEP2 && prob->kind != PERT_KIND_STEP3) return PERT_E_ARG;

@@ -654,9 +654,9 @@ class PertShard:
         (include/pert_hip.h, loop_ctl); launches of iterations after the stopping one are
         no-ops.  The host queues iterations ahead, copies the loss records back every
         ``chunk`` iterations and stops queueing once a copied record shows the stop (it is
-        at most ``chunk * depth`` iterations ahead: 64 by default, tens of ms of queued work
-        even for a 0.5 ms step, so a fit thread that waits for the GIL behind the helper
-        thread's host work does not leave the device idle).  Returns (losses, reason) with
+        at most ``chunk * depth`` iterations ahead: 64 by default).  On one rank that whole
+        loop runs inside one C call (pert_svi_run) with the GIL released, so the helper
+        thread's host work never stands between two chunks.  Returns (losses, reason) with
         reason 0 = max_iter reached, 1 = converged, 2 = NaN loss; the fit state is the one
         after the last recorded iteration, exactly as if the loop had run on the host."""
         n = int(max_iter)
@@ -674,14 +674,29 @@ class PertShard:
         st = self._state
         st.loop_ctl, st.loop_rec, st.loss_offset = _ptr(ctl), _ptr(rec), _ptr(offs)
         st.loss_const, st.rel_tol, st.min_iter = float(self.const_total), float(rel_tol), int(min_iter)
-        # one rank: a chunk of iterations is queued by ONE C call (pert_svi_steps) that releases
-        # the GIL, instead of ~3 GIL-holding calls per iteration; per-pass timing events, when
-        # asked for (pass_events), are recorded by that call around each pass
+        # one rank: the whole loop is ONE C call (pert_svi_run) that releases the GIL for the fit's
+        # duration -- a helper thread's Python work never delays the queueing of steps; with
+        # per-pass timing events (pass_events, bench.py) a chunk of iterations per C call
+        # (pert_svi_steps, the events recorded around each pass); sharded, per iteration from
+        # Python (the all-reduce sits between the reductions and Adam)
         chunked = self.allreduce is None and self._lib_chunk is not None
         b1, b2 = self.betas
         launched = 0
         pending = []
         try:
+            if chunked and self.pass_events is None:
+                ts = range(t0 + 1, t0 + n + 1)
+                ss = np.array([self.lr / (1.0 - b1 ** t) for t in ts], dtype=F32)         # as _set_hparams
+                ib = np.array([1.0 / math.sqrt(1.0 - b2 ** t) for t in ts], dtype=F32)
+                nl = ctypes.c_int32(0)
+                with self._dev():
+                    nat.check(self._lib_chunk.pert_svi_run(
+                        ctypes.byref(self._prob), ctypes.byref(st), ctypes.byref(self._hp),
+                        ss.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                        ib.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n, chunk, depth,
+                        1 if self.fused else 0, host.data_ptr(), ctypes.byref(nl), self._stream()), "pert_svi_run")
+                launched = int(nl.value)
+                n = 0                              # nothing left for the chunk loop below
             for j0 in range(0, n, chunk):
                 j1 = min(n, j0 + chunk)
                 if chunked:

@@ -216,8 +216,8 @@ int pert_adam(const pert_problem* prob, pert_state* st, const pert_adam_hparams*
  * Each step is pert_enum_step(update_shared = 1) when one_launch (steps 2/3, variant 3), else
  * pert_enum_pass(PERT_MODE_STEP) or pert_obs_pass, then pert_finalize and pert_adam.  With the
  * device loop armed (loop_ctl), the steps after the stopping one are no-ops.  pass_events
- * (NULL, or 2n caller-created events): events[2i] / events[2i+1] are recorded on the stream
- * around step i's pass launch (the one launch of a one_launch step), for timing.  The call
+ * (NULL, or 2n caller-created events, NULL entries skipped): events[2i] / events[2i+1] are
+ * recorded on the stream around step i's pass launch (the one launch of a one_launch step).  The call
  * only queues launches (a few microseconds each), so a binding may release its interpreter
  * lock around it.  Replaces n iterations of the svi.step loop of pert_model.py:742-758 /
  * :800-816 / :867-883 (the loss record and stopping rule stay on the device). */

@@ -325,6 +325,10 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
 #if PERT_V0_ONLINE
       // the gradient and Adam of the logits in plane pairs, packed fp32 (as enum3_kernel)
       const float S1s = S1 + o.sgm;
+      int jmax;
+      float om;
+      enum_jmax<P>(zt, o, jmax, om);
+      const float tom = S1s * om;                           // (S1 + sgm)(1 - pi_jmax), jmax_grad
       pf2 dirv2 = {0.0f, 0.0f};
       const float* mb = lds + 2 * SF;
       float* zo = st.z_pi + tile + lane;
@@ -338,7 +342,10 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
         const pf2 e1 = {em1[k0], k1 != k0 ? em1[k1] : 0.0f};
         const pf2 pk = pf2{enum_pi(o, zt[k0], k0), enum_pi(o, zt[k1], k1)};
         dirv2 += e1 * ((zz - o.zmax) - o.lse1p);
-        const pf2 gl = pk * S1s - e1 - pf2{o.gcm[k0], o.gcm[k1]};   // d(-ELBO)/dz
+        const pf2 gc = pf2{o.gcm[k0], o.gcm[k1]};
+        pf2 gl = pk * S1s - e1 - gc;                                  // d(-ELBO)/dz
+        const pf2 gj = ((S1 - e1) + (o.sgm - gc)) - tom;              // the argmax logit (jmax_grad)
+        gl = pf2{k0 == jmax ? gj.x : gl.x, k1 == jmax ? gj.y : gl.y};
         if (kStep) {
           const pf2 m0 = {mb[k0 * 64 + lane], mb[k1 * 64 + lane]};
           const pf2 v0 = {mb[ZF + k0 * 64 + lane], mb[ZF + k1 * 64 + lane]};
@@ -705,20 +712,28 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
 #endif
       float dirv = 0.0f;
       auto tail = [&](const auto* row) {
-        float em[P + 1];                                    // all loads in flight at once
-#pragma unroll
-        for (int k = 0; k <= P; ++k) em[k] = row[k];
-        const float S1s = em[P] + o.sgm;
+        // the eta row read per plane pair (an array of it live through the planes would cost the
+        // registers the argmax logit's two values need)
+        const float S1 = row[P];
+        const float S1s = S1 + o.sgm;
+        int jmax;
+        float om;
+        enum_jmax<P>(z, o, jmax, om);
+        const float tom = S1s * om;                         // (S1 + sgm)(1 - pi_jmax), jmax_grad
         // planes in pairs, packed fp32 (the exponential, square root and reciprocal per element)
         pf2 dirv2 = {0.0f, 0.0f};
         pert_static_for<0, (P + 1) / 2>([&](auto pc) {
           constexpr int k0 = 2 * decltype(pc)::value;
           constexpr int k1 = k0 + 1 < P ? k0 + 1 : k0;        // odd P: the last pair repeats plane k0
           const pf2 zz = {z[k0], z[k1]};
-          const pf2 e1 = {em[k0], k1 != k0 ? em[k1] : 0.0f};
+          const pf2 e1 = {row[k0], k1 != k0 ? row[k1] : 0.0f};
           const pf2 pk = pf2{enum_pi(o, z[k0], k0), enum_pi(o, z[k1], k1)};
           dirv2 += e1 * ((zz - o.zmax) - o.lse1p);
-          const pf2 gl = pk * S1s - e1 - pf2{o.gcm[k0], o.gcm[k1]};   // d(-ELBO)/dz
+          const pf2 gc = pf2{o.gcm[k0], o.gcm[k1]};
+          pf2 gl = pk * S1s - e1 - gc;                                  // d(-ELBO)/dz
+          // the argmax logit: jmax_grad, evaluated at the plane that holds it
+          const pf2 gj = ((S1 - e1) + (o.sgm - gc)) - tom;
+          gl = pf2{k0 == jmax ? gj.x : gl.x, k1 == jmax ? gj.y : gl.y};
           if (kStep) {
             const pf2 m0 = {s_m[k0 * 64 + lane], s_m[k1 * 64 + lane]};
             const pf2 v0 = {s_v[k0 * 64 + lane], s_v[k1 * 64 + lane]};
@@ -2323,7 +2338,8 @@ int pert_svi_steps(const pert_problem* prob, pert_state* st, const pert_adam_hpa
   pert_adam_hparams h = *hp;
   int rc = PERT_OK;
   auto mark = [&](int32_t i, int which) {
-    if (pass_events && rc == PERT_OK) rc = hip_status(hipEventRecord(pass_events[2 * i + which], stream));
+    if (pass_events && pass_events[2 * i + which] && rc == PERT_OK)
+      rc = hip_status(hipEventRecord(pass_events[2 * i + which], stream));
   };
   for (int32_t i = 0; i < n && rc == PERT_OK; ++i) {
     s.step = iter0 + i;                        // the loop record's iteration index

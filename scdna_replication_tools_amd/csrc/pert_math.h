@@ -248,7 +248,31 @@ struct EnumFwd {
   float pi[P];    // softmax(z)
   float gcm[P];   // gamma^cn_k [pi_k unclamped]
   int argmax;     // r * P + c of the joint MAP state               (infer_discrete, B.7)
+  int jmax;       // first argmax_k z_k (torch max, SoftmaxTransform)
+  float om;       // 1 - pi_jmax summed from the other states (not rounded through pi_jmax ~ 1)
 };
+
+// d(-ELBO)/dz of the argmax logit as minus the sum of the other logits' (a softmax gradient
+// sums to zero over the states):
+//   sum_{k != jmax} (W_k + gcm_k) - (S1 + sgm) (1 - pi_jmax),   W = eta - 1, S1 = sum W,
+// with 1 - pi_jmax = om summed from the other states.  This is the value the reference's fp32
+// autograd delivers through SoftmaxTransform's max subtraction (transforms.py:951-954: the
+// gradient of the max term lands on the argmax logit and cancels the rounding of the direct
+// path), and it stays accurate where fp32 pi_jmax has rounded to 1: the per-element form
+// pi_k (S1 + sgm) - W_k - gcm_k quantises W (1 - pi_jmax) to multiples of W eps32 there and
+// stops the prior's pull on a saturated state (tools/stop_probe.py: a fit with that form
+// stops 27 iterations later than the reference's on the genome-length fixture).
+template <int P>
+PERT_HD float jmax_grad(int jmax, const float (&em)[P + 1], const float* gcm, float sgm, float om) {
+  float wj = 0.0f, gj = 0.0f;
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    wj = (k == jmax) ? em[k] : wj;
+    gj = (k == jmax) ? gcm[k] : gj;
+  }
+  const float S1 = em[P];
+  return ((S1 - wj) + (sgm - gj)) - (S1 + sgm) * om;
+}
 
 template <int P, bool WANT_GRAD, bool WANT_ARGMAX>
 PERT_HD void enum_forward(float x, float invx, const float (&z)[P], float log1m_lam, float D,
@@ -277,6 +301,8 @@ PERT_HD void enum_forward(float x, float invx, const float (&z)[P], float log1m_
   const float lse1p = log1p_corr(t, inv1t);
   o.zmax = m;
   o.lse1p = lse1p;
+  o.jmax = jmax;
+  o.om = t * inv1t;
   // joint scores s(c, r): r-major like the oracle's (2, P) layout
   float s[2 * P];
   uint32_t mk = 0;
@@ -412,6 +438,24 @@ struct EnumOnline {
   float gcm[P];   // gamma^cn_k [pi_k unclamped]
   int argmax;     // r * P + c of the joint MAP state (first maximum)
 };
+
+// The argmax logit (first maximum, as torch's max) and 1 - pi_jmax summed from the other
+// states (jmax_grad), from the logits and the EnumOnline summary -- evaluated where the
+// gradient is formed (the passes' tails), so neither is live through the NB chains.
+template <int P>
+PERT_HD void enum_jmax(const float (&z)[P], const EnumOnline<P>& o, int& jmax, float& om) {
+  float m = z[0];
+  jmax = 0;
+#pragma unroll
+  for (int k = 1; k < P; ++k) {
+    jmax = z[k] > m ? k : jmax;
+    m = fmaxf(m, z[k]);
+  }
+  float t = 0.0f;
+#pragma unroll
+  for (int k = 0; k < P; ++k) t += (k == jmax) ? 0.0f : fexp2(fmaf(z[k], kLog2e, -o.zmaxS));
+  om = t * o.inv1t;
+}
 
 // pi_k from the EnumOnline summary (the exponential enum_online summed)
 template <int P>
@@ -619,11 +663,17 @@ template <int P>
 PERT_HD float enum_tail(const EnumFwd<P>& o, const float (&z)[P], const float (&em1)[P], float S1,
                         float (&gz)[P]) {
   float dirv = 0.0f;
+  float em[P + 1];
 #pragma unroll
   for (int k = 0; k < P; ++k) {
     dirv += em1[k] * ((z[k] - o.zmax) - o.lse1p);
     gz[k] = em1[k] - o.pi[k] * S1 + o.gcm[k] - o.pi[k] * o.sgm;
+    em[k] = em1[k];
   }
+  em[P] = S1;
+  const float gj = -jmax_grad<P>(o.jmax, em, o.gcm, o.sgm, o.om);
+#pragma unroll
+  for (int k = 0; k < P; ++k) gz[k] = (k == o.jmax) ? gj : gz[k];
   return dirv;
 }
 

@@ -41,7 +41,7 @@ import torch
 
 from . import prep
 from ._native import KIND_STEP1, KIND_STEP2, KIND_STEP3
-from .engine import EtaCodebook, PertShard
+from .engine import CanonicalPiBlock, EtaCodebook, PertShard
 from .init import init_params
 from .sharding import cell_bounds, make_allreduce
 from .tau_init import default_threads, guess_times_batched
@@ -452,6 +452,9 @@ class pert_infer_scRT():
             phases.append((name, round(time.perf_counter() - t_all, 4)))
 
         try:
+            # step 1's canonical pi trajectory (data independent, ~0.2 ms of host work per
+            # iteration): computed on the helper while the fit thread prepares the inputs
+            helper.submit(CanonicalPiBlock.precompute, P, self.learning_rate, self.max_iter_step1 + 1)
             fut_prof = []
             tic = time.perf_counter()
             inp = self._prepare(on_g1_sorted=lambda t, k: fut_prof.append(helper.submit(on_device, consensus, t, k)))

@@ -12,6 +12,8 @@ per-element arithmetic, and prints where pert_model.py:807-811's rule stops each
   detach_max   SoftmaxTransform with its max detached (mathematically the same gradient;
                in fp32 the softmax backward's residue sum_k dL/dp_k p_k no longer lands on
                the argmax logit)
+  exp64        SoftmaxTransform's exponential correctly rounded (through fp64): the same
+               fp32 autograd structure with other last bits in pi
 
 Run under ``ATEN_CPU_CAPABILITY=default|avx2|avx512`` for the reference's own fp32 arithmetic
 on CPUs with other vector units (torch CPU picks its exp / log / reduction kernels by ISA).
@@ -19,6 +21,7 @@ on CPUs with other vector units (torch CPU picks its exp / log / reduction kerne
     python tools/stop_probe.py ref [--threads 4] [--out file.npz]
 """
 import argparse
+import math
 import os
 import sys
 import time
@@ -46,6 +49,79 @@ def _patch(variant):
             probs = (x - x.max(-1, True)[0].detach()).exp()
             return probs / probs.sum(-1, True)
         SoftmaxTransform._call = _call
+    elif variant == "exp64":
+        from torch.distributions.transforms import SoftmaxTransform
+
+        def _call(self, x):
+            probs = (x - x.max(-1, True)[0]).double().exp().float()   # correctly rounded exp
+            return probs / probs.sum(-1, True)
+        SoftmaxTransform._call = _call
+    elif variant.startswith("product"):
+        # the pi site's forward values as the reference computes them, its gradient as the
+        # product's kernel forms it: d(-ELBO)/dz_k = pi_k (S1 + sum_j gcm_j) - W_k - gcm_k with
+        # gcm_k = gamma_k * mask_k; "_domfix": the argmax logit's gradient as minus the sum of
+        # the others (what the reference's max path gives); "_refmask": the clamp masks of
+        # clamp_probs(pi / sum pi) in fp32 (the reference's), not in log space
+        domfix = "domfix" in variant
+        refmask = "refmask" in variant
+        eps = float(torch.finfo(torch.float32).eps)
+
+        class PiSite(torch.autograd.Function):
+            @staticmethod
+            def forward(ctx, z, W):
+                mx = z.max(-1, True)[0]
+                p = (z - mx).exp()
+                pi = p / p.sum(-1, True)
+                pi2 = pi / pi.sum(-1, keepdim=True)
+                lc = torch.log(pi2.clamp(min=eps, max=1 - eps))
+                dirv = torch.xlogy(W, pi).sum(-1)
+                if refmask:
+                    mask = (pi2 >= eps) & (pi2 <= 1 - eps)
+                else:
+                    lz = torch.log_softmax(z, -1)
+                    mask = (lz >= math.log(eps)) & (lz <= math.log1p(-eps))
+                ctx.save_for_backward(z, W, mask)
+                return dirv, lc
+
+            @staticmethod
+            def backward(ctx, g_dir, g_lc):
+                z, W, mask = ctx.saved_tensors
+                gcm = torch.where(mask, -g_lc, torch.zeros_like(g_lc))          # gamma_k [unclamped]
+                pk = torch.softmax(z, -1)
+                S1 = W.sum(-1, keepdim=True)
+                gl = pk * (S1 + gcm.sum(-1, keepdim=True)) - W - gcm               # d(-ELBO)/dz
+                if domfix:
+                    jm = z.argmax(-1, keepdim=True)
+                    others = gl.scatter(-1, jm, torch.zeros_like(jm, dtype=gl.dtype)).sum(-1, keepdim=True)
+                    gl = gl.scatter(-1, jm, -others)
+                return gl * (-g_dir).unsqueeze(-1), None
+
+        def elbo(prob, z, **kw):
+            c = po.constrain(prob.kind, z)
+            e = prob.etas
+            dirv, lc = PiSite.apply(z["expose_pi"], e - 1.0)
+            orig_dir, orig_cat = po.Dirichlet, po.Categorical
+
+            class _Dir:                                   # Dirichlet(etas).log_prob(pi) -> site value
+                def __init__(self, conc):
+                    self.conc = conc
+
+                def log_prob(self, value):
+                    return dirv + torch.lgamma(self.conc.sum(-1)) - torch.lgamma(self.conc).sum(-1)
+
+            class _Cat:                                   # Categorical(pi).log_prob(cn) -> lc permuted
+                def __init__(self, probs):
+                    pass
+
+                def log_prob(self, value):
+                    return lc.permute(2, 0, 1)
+            po.Dirichlet, po.Categorical = _Dir, _Cat
+            try:
+                terms = po.model_terms(prob, c, **kw)
+            finally:
+                po.Dirichlet, po.Categorical = orig_dir, orig_cat
+            return sum(terms.values())
+        po.elbo = elbo
     elif variant == "logsoftmax":
         base = po.elbo
 

@@ -149,14 +149,12 @@ def test_genome_length_chain_matches_oracle_fixture():
       300 iterations -- step 1 ends in an undamped oscillation (1,000 iterations, no
       convergence) in which two fp32 evaluations of the same algebra drift 4.7 % apart after
       ~307 iterations, so its whole trace is held to twice the oracle variants' spread;
-    * the stopping iteration of every fit inside the range the oracle variants stop in (fp32,
-      fp32 in another summation order, fp64: step 2 stops at 1,151 / 1,151 / 1,187), +- 2 %;
-    * decodes >= 99.9 % equal on the S cells, and on the G1/2 cells fitted in the same tau mode;
-      a G1/2 cell's step-3 posterior is bimodal (tau ~ 0, or tau ~ 1 with u about halved: a G1
-      profile fits as fully replicated) and a cell started mid-way (t_init ~ 0.47) takes either
-      mode by trajectory details (tools/genome_mode_probe.py: the product alone, with another
-      tile length -- another order of the same per-cell sums -- flips a second cell;
-      profiles/r03i_mode_probe.log) -- at most 2 of the 64 such cells may take the other mode;
+    * every fit stops at the fp32 oracle's iteration (step 2: 1,151; the pi logits' argmax
+      gradient in the reference's max-path form, tools/stop_probe.py);
+    * decodes >= 99.9 % equal on the S cells, and on the G1/2 cells fitted in the same tau
+      mode; over all G1/2 cells >= 99.9 %, or the cells fitted in the other tau mode (a G1/2
+      cell's step-3 posterior is bimodal: tau ~ 0, or tau ~ 1 with u about halved) are the
+      ones the fp32 oracle in another summation order puts there too;
     * final lambda, a, rho, tau, u within twice the oracle variants' spread."""
     from tests._configs import genome_scrt, genome_tables, input_digest
     if not os.path.exists(GENOME) or not all(os.path.exists(f) for f in GENOME_ALTS.values()):
@@ -182,16 +180,22 @@ def test_genome_length_chain_matches_oracle_fixture():
         if key == "losses_g":
             r["dev_first_%d" % STEP1_WINDOW] = _scaled_dev(prod[key], fx[key], STEP1_WINDOW)
         rep["traces"][key] = r
-        stops = [len(fx[key])] + [len(a[key]) for a in alts.values()]
-        rep["stops"][key] = {"product": len(prod[key]), "oracles": stops}
+        rep["stops"][key] = {"product": len(prod[key]), "fp32": len(fx[key]),
+                             "others": {k: len(a[key]) for k, a in alts.items()}}
     env_sites = {k: max(_sites(a, fx)[k] for a in alts.values()) for k in ("lam", "a", "rho", "tau_s", "u_s")}
     rep["sites"], rep["sites_envelope"] = _sites(prod, fx), env_sites
+
+    def mode_flips(x):                          # G1/2 cells fitted in the other tau mode than fx
+        return [int(i) for i in np.flatnonzero(np.abs(x["tau_g"] - fx["tau_g"]) >= 0.5)]
     agree_s = float(((prod["cn_s"] == fx["cn_s"]) & (prod["rep_s"] == fx["rep_s"])).mean())
-    same_mode = np.abs(prod["tau_g"] - fx["tau_g"]) < 0.5
-    flipped = [int(i) for i in np.flatnonzero(~same_mode)]
+    flipped = mode_flips(prod)
+    same_mode = np.ones(len(prod["tau_g"]), bool)
+    same_mode[flipped] = False
     agree_g = float(((prod["cn_g"] == fx["cn_g"]) & (prod["rep_g"] == fx["rep_g"]))[:, same_mode].mean())
     rep.update(cn_s_agree=agree_s, cn_g_agree_same_mode=agree_g, g1_mode_flips=flipped,
                g1_mode_flips_t_init=[float(fx["t_init_g"][i]) for i in flipped],
+               # the flips between the fp32 oracle and the same algebra in another summation order
+               g1_mode_flips_chunked_oracle=mode_flips(alts["chunked"]),
                cn_g_agree_all=float(((prod["cn_g"] == fx["cn_g"]) & (prod["rep_g"] == fx["rep_g"])).mean()))
     from tests import _bounds
     _bounds.write_report("genome_chain_64x64x5451", rep)
@@ -203,13 +207,15 @@ def test_genome_length_chain_matches_oracle_fixture():
             assert r["dev"] <= 2 * r["envelope"], (key, r)
         else:
             assert r["dev"] <= 1e-4, (key, r)
+    # every fit stops at the fp32 reference's iteration (step 2: 1,151)
     for key, r in rep["stops"].items():
-        lo, hi = min(r["oracles"]), max(r["oracles"])
-        assert lo - 0.02 * lo <= r["product"] <= hi + 0.02 * hi, (key, r)
+        assert r["product"] == r["fp32"], (key, r)
     for k, v in rep["sites"].items():
         assert v <= 2 * env_sites[k] + 1e-6, (k, v, env_sites[k])
     assert agree_s >= 0.999, agree_s
     assert agree_g >= 0.999, agree_g
-    assert len(flipped) <= 2 and all(0.3 <= t <= 0.7 for t in rep["g1_mode_flips_t_init"]), rep
+    # G1/2 decodes: >= 99.9 % overall, or the product's tau-mode flips are the ones the
+    # reference's own algebra in another summation order makes
+    assert rep["cn_g_agree_all"] >= 0.999 or flipped == rep["g1_mode_flips_chunked_oracle"], rep
     m = out[0].merge(truth, on=['cell_id', 'chr', 'start'])
     assert (m['model_cn_state'] == m['true_somatic_cn']).mean() > 0.99

@@ -14,6 +14,15 @@ per-element arithmetic, and prints where pert_model.py:807-811's rule stops each
                the argmax logit)
   exp64        SoftmaxTransform's exponential correctly rounded (through fp64): the same
                fp32 autograd structure with other last bits in pi
+  product      the reference's forward values with the product kernel's pi-logit gradient
+               pi_k (S1 + sum gcm) - W_k - gcm_k (clamp masks in log space); "_domfix": the
+               argmax logit's gradient as minus the others' sum (the reference's max path),
+               "_refmask": the clamp masks of clamp_probs(pi / sum pi) in fp32
+
+Results (profiles/r04_stop_probe.log): ref at 4 threads and under ATEN_CPU_CAPABILITY=avx2
+stop at 1,151 like the fixture; detach_max at 1,151; logsoftmax -- whose gradient quantises
+W (1 - pi_argmax) like the product's per-element form once fp32 pi_argmax rounds to 1 -- at
+1,178, where the product stopped; product_domfix (and _refmask) at 1,151.
 
 Run under ``ATEN_CPU_CAPABILITY=default|avx2|avx512`` for the reference's own fp32 arithmetic
 on CPUs with other vector units (torch CPU picks its exp / log / reduction kernels by ISA).

@@ -81,14 +81,16 @@ def consensus_profiles(cn_g1: pd.DataFrame, col_name, clone_col='clone_id', cell
         out, keys, _, _ = prep._block_table(cn_g1, lay, None, col_name, cn_state_col, cell_col, chr_col, start_col)
         prof = prep.consensus_clone_profiles(out, col_name, clone_col=clone_col, cell_col=cell_col, chr_col=chr_col,
                                              start_col=start_col, cn_state_col=cn_state_col, keys=keys)
-        if not isinstance(cn_g1[chr_col].dtype, pd.CategoricalDtype):
-            # the caller's chromosome labels (not the sorted copy's categories), sorted as
-            # pivot_table sorts them
-            idx = prof.index
-            prof.index = pd.MultiIndex.from_arrays(
-                [np.asarray(idx.get_level_values(0), dtype=object), idx.get_level_values(1)], names=idx.names)
-            prof = prof.sort_index()
-        return prof
+        # the caller's chromosome labels (the sorted copy carries them as CHR_ORDER strings):
+        # integer labels stay integers, a categorical column keeps its own categories; sorted
+        # as pivot_table sorts them
+        col = cn_g1[chr_col]
+        lab = {str(v): v for v in pd.unique(col.dropna())}
+        idx = prof.index
+        vals = [lab.get(str(v), v) for v in idx.get_level_values(0)]
+        lev0 = pd.Categorical(vals, dtype=col.dtype) if isinstance(col.dtype, pd.CategoricalDtype) else pd.Index(vals)
+        prof.index = pd.MultiIndex.from_arrays([lev0, idx.get_level_values(1)], names=idx.names)
+        return prof.sort_index()
     return prep.consensus_clone_profiles(cn_g1, col_name, clone_col=clone_col, cell_col=cell_col, chr_col=chr_col,
                                          start_col=start_col, cn_state_col=cn_state_col)
 

@@ -267,6 +267,28 @@ def test_scrt_consensus_block_path_equals_general_path():
         pd.testing.assert_frame_equal(a, b)
 
 
+@pytest.mark.parametrize("kind", ["int", "categorical"])
+def test_scrt_consensus_block_path_keeps_caller_chr_labels(kind):
+    """Integer chromosome labels stay integers in numeric order, a categorical chr column keeps
+    its own categories -- as the general path (pivot_table) returns them -- over several
+    chromosomes (the block path sorts a copy whose labels are CHR_ORDER strings)."""
+    from scdna_replication_tools_amd.infer_scRT import consensus_profiles
+    from scdna_replication_tools_amd.simulator import simulate, to_long_form
+    sim = simulate(n_s=2, n_g=12, n_bins=5451, num_reads=5451 * 50, seed=5, n_clones=2)
+    _, df_g = to_long_form(sim, n_libs=1, copy_from="reads")
+    df_g = df_g[~df_g["chr"].astype(str).isin(["X", "Y"])].reset_index(drop=True)   # integer-labelled autosomes
+    assert df_g["chr"].nunique() > 10
+    if kind == "int":
+        df_g["chr"] = df_g["chr"].astype(str).astype(np.int64)
+    else:
+        cats = sorted(df_g["chr"].astype(str).unique()) + ["MT"]
+        df_g["chr"] = pd.Categorical(df_g["chr"].astype(str), categories=cats)
+    assert prep._block_layout(df_g, "cell_id", "chr", "start", None) is not None
+    a = prep.consensus_clone_profiles(df_g, "copy", clone_col="clone_id", cn_state_col="state")
+    b = consensus_profiles(df_g, "copy", clone_col="clone_id", cn_state_col="state")
+    pd.testing.assert_frame_equal(a, b)
+
+
 def test_pivot_any_block_path_equals_general_pivot():
     from scdna_replication_tools_amd.simulator import simulate, to_long_form
     sim = simulate(n_s=4, n_g=30, n_bins=300, num_reads=300 * 183, seed=6)

@@ -137,3 +137,51 @@ def test_enum_cellbin_host_matches_autograd(nat, P):
     assert rel(out["gt"], pt.grad.numpy() * phi * (1 - phi)) < 1e-5
     idx = torch.argmax(lp.reshape(2 * P, n), 0).numpy()
     assert (out["argmax"] == idx).mean() > 0.99
+
+
+def test_argmax_logit_gradient_at_saturation(nat):
+    """Once the prior has pushed a state so far that fp32 pi_argmax rounds to 1, the
+    reference's fp32 autograd (SoftmaxTransform + Dirichlet + Categorical, the oracle's
+    tensor algebra) still delivers the prior's pull W (1 - pi_argmax) on the argmax logit --
+    through the gradient of the max subtraction, minus the other logits' sum -- and so do the
+    kernels (pert_math.h jmax_grad).  The per-element form pi_k (S1 + sgm) - W_k - gcm_k rounds
+    that pull to 0 here (tools/stop_probe.py: why the product's genome-length step 2 stopped 27
+    iterations late)."""
+    from torch.distributions import (Bernoulli, Categorical, Dirichlet, NegativeBinomial, constraints,
+                                      transform_to)
+    P, n = 13, 400
+    rng = np.random.default_rng(7)
+    x = rng.integers(50, 300, n).astype(np.float32)
+    st = rng.integers(0, P, n)
+    W = np.float32(1e6 - 1)
+    em1 = np.zeros((n, P), np.float32)
+    em1[np.arange(n), st] = W
+    S1 = em1.sum(1)
+    z = (rng.normal(size=(n, P)) * 0.5).astype(np.float32)
+    z[np.arange(n), st] += rng.uniform(17.5, 21.0, n).astype(np.float32)      # fp32 pi_argmax ~ 1
+    D = rng.uniform(20, 60, n).astype(np.float32)
+    phi = rng.uniform(0.01, 0.99, n).astype(np.float32)
+    lam = 0.75
+    out = nat.selftest_enum_cellbin_host(P, x, em1, S1, z, np.log1p(-lam), D, phi)
+
+    # the reference's arithmetic: fp32 torch autograd of the model's terms (oracle/pert_oracle.py)
+    zt = torch.tensor(z, requires_grad=True)
+    pi = transform_to(constraints.simplex)(zt)
+    X = torch.tensor(x)
+    cn = torch.arange(P).reshape(P, 1)
+    rep = torch.tensor([0., 1.]).reshape(2, 1, 1)
+    delta = torch.clamp(cn * (1 + rep) * torch.tensor(D), min=1.0)
+    lp = (Categorical(pi).log_prob(cn) + Bernoulli(torch.tensor(phi)).log_prob(rep)
+          + NegativeBinomial(delta, probs=torch.tensor(lam)).log_prob(X))
+    E = torch.logsumexp(lp.reshape(2 * P, n), 0)
+    (E.sum() + Dirichlet(torch.tensor(em1) + 1.0).log_prob(pi).sum()).backward()
+    i = np.arange(n)
+    ref = zt.grad.numpy()[i, st]
+    pull = (np.float64(W) * (1.0 - torch.softmax(torch.tensor(z, dtype=torch.float64), -1).numpy()))[i, st]
+    assert (pi.detach().numpy()[i, st] == 1.0).mean() > 0.6          # saturated in fp32
+    assert np.median(pull) > 1e-2                                    # and the pull is not small
+    got = out["gz"][i, st]
+    assert np.abs(got - ref).max() < 2e-4, np.abs(got - ref).max()
+    # the per-element form's value on these elements misses the pull
+    old = (em1 - torch.softmax(torch.tensor(z), -1).numpy() * S1[:, None])[i, st]
+    assert np.abs(old - ref).max() > 50 * 2e-4

@@ -135,10 +135,11 @@ def load(path: str, gil: bool = True):
             "{} not found: the PERT HIP extension is not built (run "
             "`python -m scdna_replication_tools_amd.build`). There is no CPU fallback.".format(path))
     try:
-        # PyDLL: the calls keep the GIL.  Every entry point returns in microseconds (launches,
-        # no synchronisation), and a thread that drops the GIL around each launch waits for it
-        # again behind whatever Python work another thread of the fit is doing (up to the
-        # interpreter's switch interval per call), which starves the device of queued steps.
+        # PyDLL (gil=True): the calls keep the GIL.  Those entry points return in microseconds
+        # (launches, no synchronisation), and a thread that drops the GIL around each launch
+        # waits for it again behind whatever Python work another thread of the fit is doing.
+        # The one entry point that waits on the device, pert_svi_run (a whole fit), and the
+        # chunked pert_svi_steps go through the CDLL binding (gil=False, lib_nogil()).
         handle = ctypes.PyDLL(path) if gil else ctypes.CDLL(path)
     except OSError as e:  # pragma: no cover
         raise NativeLibraryError("failed to load {}: {}".format(path, e))

@@ -77,6 +77,15 @@ PERT_HD float frcp(float x) {
 #endif
 }
 
+// every active lane of the wave (the predicate itself on the host self-test)
+PERT_HD bool wave_all(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __all(p) != 0;
+#else
+  return p;
+#endif
+}
+
 // log1p(q) for q >= 0 given inv_u ~= 1/(1+q): the rounding error of 1+q is added
 // back (q - ((1+q) - 1)) / (1+q) -- exact to a few ulp of the result.
 PERT_HD float log1p_corr(float q, float inv_u) {
@@ -147,6 +156,34 @@ PERT_HD void nb_asym_pair(pf2 chi, pf2 rchi, pf2 lchi, float D, float rD, float 
   const pf2 lu = pf2{__builtin_amdgcn_logf_or_log2(u.x), __builtin_amdgcn_logf_or_log2(u.y)} * kLn2;
   const pf2 l1 = lu + (q - (u - 1.0f)) * iu;          // log1p(x/d), log1p_corr
   const pf2 l2 = l1 + (lchi + ldx);                   // log1p(d/x)
+  const pf2 r2 = r * r, rz2 = rz * rz;
+  const pf2 sr = r * (0.0833333333333333333f - r2 * (0.00277777777777777778f - r2 * 0.000793650793650793651f));
+  const pf2 srz = rz * (0.0833333333333333333f - rz2 * (0.00277777777777777778f - rz2 * 0.000793650793650793651f));
+  const pf2 lam = (d - 0.5f) * l1 + x * l2 + (srz - sr);
+  const pf2 r4 = r2 * r2, rz4 = rz2 * rz2;
+  const pf2 psi = l1 - 0.5f * (rz - r) - 0.0833333333333333333f * (rz2 - r2)
+                  + 0.00833333333333333333f * (rz4 - r4) - 0.00396825396825396825f * (rz4 * rz2 - r4 * r2);
+  nchi = d * log1m_lam + lam;
+  bc = chi * (psi + log1m_lam);
+}
+
+// nb_asym_pair without the hoisted per-(bin, cell) invariants: each chain's own 1/d and
+// log1p(d/x) (as nb_lgdiff_asym), the series in packed fp32 -- for chain pairs of the
+// low-coverage regime whose deltas are all >= kAsymMin (no extra values live across chains).
+PERT_HD void nb_asym_pair_direct(pf2 chi, float D, float x, float invx, float log1m_lam, pf2& nchi, pf2& bc) {
+  const pf2 d = chi * D;
+  const pf2 r = {frcp(d.x), frcp(d.y)};
+  const pf2 zs = d + x;
+  const pf2 rz = {frcp(zs.x), frcp(zs.y)};
+  const pf2 q = r * x;                                // x/d
+  const pf2 iu = d * rz;                              // 1/(1 + x/d)
+  const pf2 u = q + 1.0f;
+  const pf2 lu = pf2{__builtin_amdgcn_logf_or_log2(u.x), __builtin_amdgcn_logf_or_log2(u.y)} * kLn2;
+  const pf2 l1 = lu + (q - (u - 1.0f)) * iu;          // log1p(x/d)
+  const pf2 q2 = d * invx;                            // d/x (0 when x == 0)
+  const pf2 u2 = q2 + 1.0f;
+  const pf2 lu2 = pf2{__builtin_amdgcn_logf_or_log2(u2.x), __builtin_amdgcn_logf_or_log2(u2.y)} * kLn2;
+  const pf2 l2 = lu2 + (q2 - (u2 - 1.0f)) * (rz * x); // log1p(d/x)
   const pf2 r2 = r * r, rz2 = rz * rz;
   const pf2 sr = r * (0.0833333333333333333f - r2 * (0.00277777777777777778f - r2 * 0.000793650793650793651f));
   const pf2 srz = rz * (0.0833333333333333333f - rz2 * (0.00277777777777777778f - rz2 * 0.000793650793650793651f));
@@ -524,6 +561,27 @@ PERT_HD void enum_online(float x, float invx, const float (&z)[P], float log1m_l
 #endif
       // the group's NB parts; on the asymptotic path two chains per packed-fp32 evaluation
       float nn[G], bb[G];
+      bool pdone[(G + 1) / 2];                              // (low coverage) pair taken packed
+      if constexpr (!ASYM) {
+        pert_static_for<0, (G + 1) / 2>([&](auto pc) {
+          constexpr int j0 = 2 * decltype(pc)::value, j1 = j0 + 1;
+          constexpr int i0 = g * G + j0, i1 = g * G + j1;
+          constexpr bool h0 = i0 < CL.n, h1 = j1 < G && i1 < CL.n;
+          constexpr int c0 = h0 ? CL.v[i0] : 1, c1 = h1 ? CL.v[i1] : 1;
+          pdone[decltype(pc)::value] = false;
+          if constexpr (h0 && h1 && c0 != 0) {
+            if (wave_all((float)c0 * D >= kAsymMin)) {     // both chains past the shift on every lane
+              pf2 n2, b2;
+              nb_asym_pair_direct(pf2{(float)c0, (float)c1}, D, x, invx, log1m_lam, n2, b2);
+              nn[j0] = n2.x;
+              bb[j0] = b2.x;
+              nn[j1] = n2.y;
+              bb[j1] = b2.y;
+              pdone[decltype(pc)::value] = true;
+            }
+          }
+        });
+      }
       if constexpr (ASYM) {
         pert_static_for<0, (G + 1) / 2>([&](auto pc) {
           constexpr int j0 = 2 * decltype(pc)::value, j1 = j0 + 1;
@@ -545,7 +603,11 @@ PERT_HD void enum_online(float x, float invx, const float (&z)[P], float log1m_l
         constexpr int j = decltype(jc)::value;
         constexpr int idx = g * G + j;
         constexpr int jp = j - j % 2;                          // pair head
-        constexpr bool paired = ASYM && jp + 1 < G && g * G + jp + 1 < CL.n && CL.v[g * G + jp] != 0;
+        constexpr bool pairable = jp + 1 < G && g * G + jp + 1 < CL.n && CL.v[g * G + jp] != 0;
+        constexpr bool paired = ASYM && pairable;
+        if constexpr (!ASYM && pairable && idx < CL.n) {
+          if (pdone[j / 2]) return;                          // (wave-uniform)
+        }
         if constexpr (idx < CL.n && !paired) {
           constexpr int chi = CL.v[idx];
           if constexpr (chi == 0) {

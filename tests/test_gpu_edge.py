@@ -75,3 +75,19 @@ def test_empty_shard_is_refused():
     kw["libs"] = np.zeros(0, int)
     with pytest.raises(ValueError):
         PertShard(2, init=init_constrained("step2", z), device="cuda", **kw)
+
+
+def test_low_coverage_full_waves():
+    """20 kb-like coverage (~6.5 reads per bin, D = u omega (1-lam)/lam ~ 0.6-1.3) on full 64-cell
+    waves: chain pairs whose deltas are >= 5 on every lane run the series packed
+    (pert_math.h nb_asym_pair_direct), the others clamp / shift per lane -- loss, gradients and
+    decode against the fp64 oracle.  The case is checked to exercise both paths."""
+    L, N = 120, 192
+    prob, kw, z = make_problem("step2", L=L, N=N, n_libs=1, seed=11, num_reads=7.0 * L)
+    gc = np.asarray(kw["gc"], np.float64)
+    gcf = np.stack([gc ** k for k in (4, 3, 2, 1, 0)], 1)                       # (L, K1)
+    D = z["expose_u"].numpy()[None, :] * np.exp(gcf @ z["expose_betas"].numpy().T) * (1 - 0.75) / 0.75
+    wave_min = D.reshape(L, N // 64, 64).min(-1)                                # per bin and wave
+    assert (10 * wave_min >= 5).mean() > 0.5          # the chi >= 10 pairs pack on most wave-bins
+    assert (2 * wave_min < 5).all()                   # the chi = 2 .. 4 chains shift everywhere
+    _check("step2", prob, kw, z)

@@ -699,6 +699,14 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
     EnumOnline<P> o;
     enum_online<P, kEnum3Group, !kDecode, kDecode>(x, invx, z, log1m_lam, D, phi, o);
 
+    // The copies of bin l+1 (issued at the top of this bin) land in the buffers the next
+    // iteration reads first, with no wait of their own: hipcc's LDS-DMA tracking does not carry
+    // them across the loop's back edge (ROCm 7.2: no vmcnt before those reads in the GRAD and
+    // DECODE instances; the STEP instance's wait for this bin's Adam moments covered them).
+    // Wait here, after the NB chains have covered their latency and before this bin's stores,
+    // so the wait never includes a store (the register operands pin it after the forward pass).
+    if (kDecode) asm volatile("s_waitcnt vmcnt(0)" :: "v"(o.E), "v"(o.argmax) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" :: "v"(o.E), "v"(o.sgm), "v"(o.gt) : "memory");
     float gtv = 0.0f;
     if (kDecode) {
       st.cn_out[(size_t)l * ldn + n] = (uint8_t)(o.argmax % P);
@@ -2397,7 +2405,7 @@ int pert_svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hpara
   }
   const hipError_t e = hipStreamSynchronize(stream);     // every queued launch and copy
   if (rc == PERT_OK) rc = hip_status(e);
-  for (int k = 0; k < made; ++k) hipEventDestroy(ev[k]);
+  for (int k = 0; k < made; ++k) (void)hipEventDestroy(ev[k]);
   return rc;
 }
 

@@ -494,6 +494,7 @@ class pert_infer_scRT():
             c1 = s1.constrained()
             lambda_fit = np.asarray(c1["expose_lambda"], dtype=np.float32)
             beta_means_fit = np.asarray(c1["expose_beta_means"], dtype=np.float32)
+            self.step1_sites = {"lambda": lambda_fit, "beta_means": beta_means_fit}     # for inspection
             del s1
             mark("step1")
 

@@ -139,6 +139,8 @@ def product_arrays(m, cn_s_out, supp_s, cn_g1_out, supp_g1) -> dict:
                cn_s=grid(cn_s_out, inp.cells_s, "model_cn_state", np.uint8),
                rep_s=grid(cn_s_out, inp.cells_s, "model_rep_state", np.uint8),
                tau_s=per_cell(cn_s_out, inp.cells_s, "model_tau"), u_s=per_cell(cn_s_out, inp.cells_s, "model_u"))
+    if getattr(m, "step1_sites", None) is not None:          # the product's step-1 fit (diagnostics)
+        out["beta_means"] = np.asarray(m.step1_sites["beta_means"], np.float32)
     rho = np.zeros(L, np.float32)
     rho[loci_index(inp).get_indexer(loci_keys(cn_s_out, m))] = cn_s_out["model_rho"].to_numpy(np.float32)
     out["rho"] = rho

@@ -96,6 +96,15 @@ def test_c4_full_size_pass_per_cell_and_shared_parity():
     full = PertShard(2, reads, sim.gc, libs, 1, 13, 4, init, eta=eta, **common)
     cells = np.r_[0:8, 4996:5004, 9992:10000]
     loss, g = full.loss_and_grads(pi_cells=cells)
+    # the pass is deterministic: a second launch on the same state gives the same bits (each
+    # bin's LDS-DMA copies waited for before they are read)
+    loss2, g2 = full.loss_and_grads(pi_cells=cells)
+    assert loss2 == loss
+    for name in ("expose_rho", "expose_a", "expose_pi", "expose_u"):
+        assert np.array_equal(np.asarray(g2[name]), np.asarray(g[name])), name
+    cn1, rep1 = full.decode()
+    cn2, rep2 = full.decode()
+    assert torch.equal(cn1, cn2) and torch.equal(rep1, rep2)
     zc = full.unconstrained(pi_cells=cells)
     # oracle on the sampled cells at the same point (the per-cell sites depend on the shared
     # ones and on their own cells only)

@@ -91,3 +91,43 @@ def test_low_coverage_full_waves():
     assert (10 * wave_min >= 5).mean() > 0.5          # the chi >= 10 pairs pack on most wave-bins
     assert (2 * wave_min < 5).all()                   # the chi = 2 .. 4 chains shift everywhere
     _check("step2", prob, kw, z)
+
+
+def test_saturated_pi_argmax_gradient():
+    """A g1_clones-weight prior (eta = 1e6 on one state) and pi logits pushed so far that fp32
+    pi_argmax rounds to 1 (the late iterations of a genome-length step 2): the pass must keep
+    the prior's pull W (1 - pi_argmax) on the argmax logit -- the reference's fp32 autograd
+    delivers it through the max subtraction (pert_math.h jmax_grad) -- where the per-element
+    form pi_k (S1 + sgm) - W_k - gcm_k rounds it to multiples of W ulp(1)."""
+    import torch
+    L, N, P = 48, 64, 13
+    prob, kw, z = make_problem("step2", L=L, N=N, n_libs=1, seed=13, prior="clone")
+    st = prob.etas.numpy().argmax(-1)                                         # (L, N)
+    rng = np.random.default_rng(5)
+    zp = z["expose_pi"].numpy().copy()
+    boost = rng.uniform(13.5, 17.0, (L, N)).astype(np.float32)
+    np.put_along_axis(zp, st[..., None], np.take_along_axis(zp, st[..., None], 2) + boost[..., None], axis=2)
+    z = dict(z, expose_pi=torch.tensor(zp.astype(np.float32).astype(np.float64)))
+    # the reference's fp32 arithmetic (its clamp_probs at fp32 eps cuts the Categorical's path
+    # on the elements whose pi rounds above 1 - eps; fp64 keeps it)
+    _, ref32 = po.loss_and_grads(prob.to(torch.float32), {k: v.float() for k, v in z.items()})
+    loss, g = _shard("step2", kw, z).loss_and_grads()
+    pi32 = torch.softmax(torch.tensor(zp, dtype=torch.float32), -1).numpy()
+    assert (np.take_along_axis(pi32, st[..., None], 2) == 1.0).mean() > 0.5      # saturated in fp32
+    pull = np.take_along_axis(1e6 * (1.0 - torch.softmax(torch.tensor(zp), -1).numpy()), st[..., None], 2)
+    assert np.median(pull) > 5e-2                 # the per-element form misses ~0.06 (median) of it
+    got = np.take_along_axis(np.asarray(g["expose_pi"], np.float64), st[..., None], 2)
+    ref = np.take_along_axis(ref32["expose_pi"].double().numpy(), st[..., None], 2)
+    err = np.abs(got - ref)
+    assert np.median(err) < 2e-3 and np.quantile(err, 0.99) < 1e-2, (np.median(err), np.quantile(err, 0.99))
+    # the loss against the fp64 oracle with clamp_probs at the fp32 eps (as the reference's fp32
+    # Categorical clamps; the saturated pi_k ~ e^-17 of the other states sit below it)
+    import torch.distributions.utils as tdu
+    orig = tdu.clamp_probs
+    eps = float(torch.finfo(torch.float32).eps)
+    tdu.clamp_probs = lambda p: p.clamp(min=eps, max=1 - eps)
+    try:
+        ref_loss32eps, _ = po.loss_and_grads(prob, z)
+    finally:
+        tdu.clamp_probs = orig
+    assert abs(loss - float(ref_loss32eps)) <= 2e-5 * abs(float(ref_loss32eps)), (loss, float(ref_loss32eps))

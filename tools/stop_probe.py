@@ -153,6 +153,9 @@ def main():
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--max-iter", type=int, default=None)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--step1-from", default=None,
+                    help="an .npz holding lam (and beta_means): start step 2 from those step-1 sites "
+                         "instead of the fixture's (e.g. the product's dump of the same chain)")
     a = ap.parse_args()
     torch.set_num_threads(a.threads)
     _patch(a.variant)
@@ -166,6 +169,11 @@ def main():
                                              keys=inp.keys_g)
     etas = m._build_etas(inp, profiles)
     lam, bm, t_init = fx["lam"], fx["beta_means"], fx["t_init_s"]
+    if a.step1_from:
+        alt = dict(np.load(a.step1_from))
+        lam = np.asarray(alt["lam"], np.float32).reshape(np.shape(lam))
+        if "beta_means" in alt:
+            bm = np.asarray(alt["beta_means"], np.float32).reshape(np.shape(bm))
     dt = torch.float32
     ploidy = etas.argmax_states().astype(np.float32).mean(0)
     L, N = inp.reads_s.shape

@@ -143,6 +143,23 @@ def _patch(variant):
             return sum(terms.values())
         po.elbo = elbo
         assert base is not po.elbo
+    elif variant == "contdir":
+        # the reference's arithmetic for the gradient, but the Dirichlet site's VALUE in the
+        # loss record without the reference's per-element fp32 rounding: (eta - 1) log pi summed
+        # and the normaliser added in fp64 (what a kernel with an fp64 accumulator records)
+        base = po.elbo
+
+        def elbo(prob, z, **kw):
+            c = po.constrain(prob.kind, z)
+            terms = po.model_terms(prob, c, **kw)
+            e = prob.etas.double()
+            zp = z["expose_pi"].double()
+            cont = ((e - 1.0) * torch.log_softmax(zp, -1)).sum() + (torch.lgamma(e.sum(-1)) - torch.lgamma(e).sum(-1)).sum()
+            ref = terms["expose_pi"]
+            total = sum(terms.values())
+            return total + (cont - ref.double()).detach().to(total.dtype)
+        po.elbo = elbo
+        assert base is not po.elbo
     elif variant != "ref":
         raise SystemExit("unknown variant " + variant)
 

@@ -284,7 +284,7 @@ def main():
     ap.add_argument("--prior", default="g1_clones", choices=["g1_clones", "g1_composite"],
                     help="CN prior of the step-2 fit: g1_clones (the tutorial's; one code per clone state) or "
                          "g1_composite (the reference's default; the product's composite code book, many rows)")
-    ap.add_argument("--event-stride", type=int, default=1,
+    ap.add_argument("--event-stride", type=int, default=5,
                     help="HIP events around the pass of every k-th timed step (1: every step)")
     ap.add_argument("--cpu-cells", type=int, default=640)
     ap.add_argument("--cpu-steps", type=int, default=3)
@@ -383,6 +383,9 @@ def main():
     # chunks, with no per-step host synchronisation.
     if args.warmup > 0:
         shard.run_svi(args.warmup, min_iter=10 ** 9, rel_tol=0.0)
+    # the loop's buffers (and step 1's canonical pi trajectory) set up before the timed region,
+    # as run_pert_model has them ready before a fit starts
+    shard.reserve_svi(args.steps)
     if pg is not None:
         pg.barrier()
     torch.cuda.synchronize()

@@ -23,7 +23,10 @@
  *   reads      float  [L][ldn]     integer-valued counts
  *   gcf        float  [L][K1]      [gc^K .. gc^1, 1] (make_gc_features, pert_model.py:460-463)
  *   eta_code   uint16 [L][ldn]     row index into eta_table          (steps 2/3)
- *   eta_table  float  [n_codes][P+1]  (eta_k - 1 for k < P, then S1 = sum_k (eta_k - 1))
+ *   eta_table  float  [n_codes][P+2]  eta_k - 1 for k < P, then S1 = sum_k (eta_k - 1), then
+ *                                   A = fp32 lgamma(sum_k eta_k) as torch evaluates it: each
+ *                                   element's Dirichlet value is rounded to A's grid as the
+ *                                   reference's fp32 log_prob rounds it (0: not rounded)
  *   z_pi/m_pi/v_pi/g_pi float [ldn/64][L][P][64]  softmax logits of expose_pi and Adam
  *                                   moments in wave tiles: cell n, state k of bin l at
  *                                   (((n/64)*L + l)*P + k)*64 + n%64  (a wave streams one

@@ -33,6 +33,9 @@ constexpr int kMaxLT = 64;
 constexpr int kShortLT3 = 12;                    // variant 3's tile length on multi-round launches
 constexpr int kLongLT3 = 18;                     // ... and on launches of 8 rounds or more
 constexpr int kEtaLdsFloats = 1024;   // eta tables up to 4 KB are staged in LDS
+// eta table row: eta_k - 1 (k < P), S1 = sum_k (eta_k - 1), A = fp32 lgamma(sum eta) (the grid
+// the reference's fp32 Dirichlet value is rounded to; 0: unrounded) -- include/pert_hip.h
+__host__ __device__ constexpr int kTabRow(int P) { return P + 2; }
 constexpr int kBlkSlots = 4;      // loss, d/da, sum delta, sum gdd (step 1)
 constexpr float kHalfLog2PiF = 0.918938533204672742f;
 
@@ -172,11 +175,11 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
   // large composite prior): the tail's per-lane row gather is then an LDS read, not a
   // dependent global load after the forward pass
   float* s_tab = s_bc + LT * (K1 + 1);
-  const bool etal = !kDecode && pr.n_codes * (P + 1) <= kEtaLdsFloats;
+  const bool etal = !kDecode && pr.n_codes * kTabRow(P) <= kEtaLdsFloats;
   // Tile prologue: every load below is unconditional (clamped index, masked store), so each
   // group is one round trip instead of one guarded load + wait per loop trip.
   if (etal) {
-    const int nt = pr.n_codes * (P + 1);
+    const int nt = pr.n_codes * kTabRow(P);
     float tv[kEtaLdsFloats / 64];
 #pragma unroll
     for (int r = 0; r < kEtaLdsFloats / 64; ++r) tv[r] = pr.eta_table[min(lane + 64 * r, nt - 1)];
@@ -310,17 +313,19 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
       float zt[P];
 #pragma unroll
       for (int k = 0; k < P; ++k) zt[k] = sb[k * 64 + lane];
-      float em1[P], S1;
+      float em1[P], S1, Arow;
       if (etal) {
-        const float* row = s_tab + code * (P + 1);
+        const float* row = s_tab + code * kTabRow(P);
 #pragma unroll
         for (int k = 0; k < P; ++k) em1[k] = row[k];
         S1 = row[P];
+        Arow = row[P + 1];
       } else {
-        const float* row = pr.eta_table + (size_t)code * (P + 1);
+        const float* row = pr.eta_table + (size_t)code * kTabRow(P);
 #pragma unroll
         for (int k = 0; k < P; ++k) em1[k] = row[k];
         S1 = row[P];
+        Arow = row[P + 1];
       }
 #if PERT_V0_ONLINE
       // the gradient and Adam of the logits in plane pairs, packed fp32 (as enum3_kernel)
@@ -329,6 +334,7 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
       float om;
       enum_jmax<P>(zt, o, jmax, om);
       const float tom = S1s * om;                           // (S1 + sgm)(1 - pi_jmax), jmax_grad
+      const float lpj = ref_log_pi_jmax<P>(zt, o.zmax, jmax);
       pf2 dirv2 = {0.0f, 0.0f};
       const float* mb = lds + 2 * SF;
       float* zo = st.z_pi + tile + lane;
@@ -341,7 +347,8 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
         const pf2 zz = {zt[k0], zt[k1]};
         const pf2 e1 = {em1[k0], k1 != k0 ? em1[k1] : 0.0f};
         const pf2 pk = pf2{enum_pi(o, zt[k0], k0), enum_pi(o, zt[k1], k1)};
-        dirv2 += e1 * ((zz - o.zmax) - o.lse1p);
+        const pf2 lp = (zz - o.zmax) - o.lse1p;
+        dirv2 += e1 * pf2{k0 == jmax ? lpj : lp.x, k1 == jmax ? lpj : lp.y};
         const pf2 gc = pf2{o.gcm[k0], o.gcm[k1]};
         pf2 gl = pk * S1s - e1 - gc;                                  // d(-ELBO)/dz
         const pf2 gj = ((S1 - e1) + (o.sgm - gc)) - tom;              // the argmax logit (jmax_grad)
@@ -368,7 +375,7 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
           if constexpr (k1 != k0) gp[k1 * 64] = g1;
         }
       });
-      const float dirv = dirv2.x + dirv2.y;
+      const float dirv = dir_site_round(dirv2.x + dirv2.y, Arow);
       if (valid) {
         loss += o.E + dirv;
         gtv = o.gt;
@@ -380,7 +387,7 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
       }
 #else
       float gz[P];
-      const float dirv = enum_tail<P>(o, zt, em1, S1, gz);
+      const float dirv = dir_site_round(enum_tail<P>(o, zt, em1, S1, gz), Arow);
       if (valid) {
         loss += o.E + dirv;
         gtv = o.gt;
@@ -480,7 +487,7 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
 #ifndef PERT_ENUM3_PRIO
 #define PERT_ENUM3_PRIO 1            // issue priority falls by quarters of the tile (0: none)
 #endif
-constexpr int kEnum3TabFloats = 192;            // eta table staged in LDS up to this size
+constexpr int kEnum3TabFloats = 256;            // eta table staged in LDS up to this size
 constexpr unsigned kRsrcWord3 = 0x00020000;     // raw buffer resource, gfx9 data format
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
@@ -561,7 +568,6 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
   __shared__ __attribute__((aligned(16))) float s_v[kStep ? ZF : 4];
   __shared__ __attribute__((aligned(16))) float s_xc[96];          // x (64 floats), code (64 x u16)
   __shared__ float s_bc[kMaxLT * (K1T + 1)];                        // per bin: rho, gcf[K1]
-  __shared__ float s_binp[kDecode ? 1 : kMaxLT];
   __shared__ float s_tab[kDecode ? 1 : kEnum3TabFloats];
 
   const int lane = threadIdx.x;
@@ -603,7 +609,7 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
   E3_DMA_Z(0u);
 
   // ---- tile prologue: eta table (when small), per-bin rho and GC features, cell parameters
-  const int ntab = pr.n_codes * (P + 1);
+  const int ntab = pr.n_codes * kTabRow(P);
   const bool etal = !kDecode && ntab <= kEnum3TabFloats;
   if (!kDecode && etal) {
     for (int i = lane; i < ntab; i += 64) s_tab[i] = pr.eta_table[i];
@@ -650,6 +656,8 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
   for (int k = 0; k < K1T; ++k) acc[k] = 0.0f;
   float sgt = 0.0f, loss = 0.0f, ga = 0.0f;
   const uint32_t voff = lane * 4;
+  // the tile's partials: coherent (sc1) stores when another workgroup of this launch reads them
+  const bool coh = kStep && fuse;
 
 #if PERT_ENUM3_PRIO
   __builtin_amdgcn_s_setprio(3);
@@ -728,6 +736,7 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
         float om;
         enum_jmax<P>(z, o, jmax, om);
         const float tom = S1s * om;                         // (S1 + sgm)(1 - pi_jmax), jmax_grad
+        const float lpj = ref_log_pi_jmax<P>(z, o.zmax, jmax);   // the reference's fp32 log pi_jmax
         // planes in pairs, packed fp32 (the exponential, square root and reciprocal per element)
         pf2 dirv2 = {0.0f, 0.0f};
         pert_static_for<0, (P + 1) / 2>([&](auto pc) {
@@ -736,7 +745,8 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
           const pf2 zz = {z[k0], z[k1]};
           const pf2 e1 = {row[k0], k1 != k0 ? row[k1] : 0.0f};
           const pf2 pk = pf2{enum_pi(o, z[k0], k0), enum_pi(o, z[k1], k1)};
-          dirv2 += e1 * ((zz - o.zmax) - o.lse1p);
+          const pf2 lp = (zz - o.zmax) - o.lse1p;
+          dirv2 += e1 * pf2{k0 == jmax ? lpj : lp.x, k1 == jmax ? lpj : lp.y};
           const pf2 gc = pf2{o.gcm[k0], o.gcm[k1]};
           pf2 gl = pk * S1s - e1 - gc;                                  // d(-ELBO)/dz
           // the argmax logit: jmax_grad, evaluated at the plane that holds it
@@ -766,10 +776,10 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
               __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, g1), rg, voff, zoff + k1 * 256, 0);
           }
         });
-        dirv = dirv2.x + dirv2.y;
+        dirv = dir_site_round(dirv2.x + dirv2.y, row[P + 1]);   // the site value's fp32 rounding
       };
-      if (etal) tail(s_tab + code * (P + 1));
-      else tail(pr.eta_table + (size_t)code * (P + 1));
+      if (etal) tail(s_tab + code * kTabRow(P));
+      else tail(pr.eta_table + (size_t)code * kTabRow(P));
       if (valid) {
         loss += o.E + dirv;
         gtv = o.gt;
@@ -782,20 +792,17 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
       }
     }
     if (!kDecode && !frozen) {
+      // the bin's rho partial of this wave tile, stored by lane 0 (the LDS a staging row would
+      // take holds the eta table's rounding column instead)
       const float ws = wave_sum(gtv);
-      if (lane == 0) s_binp[lb] = ws;
+      if (lane == 0) {
+        float* q = st.bin_part + (size_t)wt * pr.L + l;
+        if (coh) st_coh(q, ws);
+        else *q = ws;
+      }
     }
   }
   if (kDecode) return;
-  // the tile's partials; coherent (sc1) stores when another workgroup of this launch reads them
-  const bool coh = kStep && fuse;
-  if (!frozen) {
-    for (int i = lane; i < nb; i += 64) {
-      float* q = st.bin_part + (size_t)wt * pr.L + l0 + i;
-      if (coh) st_coh(q, s_binp[i]);
-      else *q = s_binp[i];
-    }
-  }
   if (valid) {
     float* cp = st.cell_part + (size_t)blockIdx.y * (K1 + 1) * N + n;
 #pragma unroll
@@ -2037,7 +2044,7 @@ bool problem_ok(const pert_problem* p) {
 size_t dma_lds_bytes(int P, int mode, const pert_state& st, const pert_problem& pr) {
   const int ZF = P * 64, SF = ZF + 96;
   const int lt = st.bins_per_tile;
-  const int tab = (mode != PERT_MODE_DECODE && pr.n_codes * (P + 1) <= kEtaLdsFloats) ? pr.n_codes * (P + 1) : 0;
+  const int tab = (mode != PERT_MODE_DECODE && pr.n_codes * kTabRow(P) <= kEtaLdsFloats) ? pr.n_codes * kTabRow(P) : 0;
   return sizeof(float) * (size_t)(2 * SF + (mode == PERT_MODE_STEP ? 2 * ZF : 0) + lt + lt * (pr.K1 + 1) + tab);
 }
 

@@ -494,6 +494,58 @@ PERT_HD void enum_jmax(const float (&z)[P], const EnumOnline<P>& o, int& jmax, f
   om = t * o.inv1t;
 }
 
+// ---- the Dirichlet site's VALUE as the reference's fp32 arithmetic forms it
+// (torch.distributions.Dirichlet.log_prob: xlogy(eta - 1, pi).sum(-1) + lgamma(eta.sum(-1))
+//  - lgamma(eta).sum(-1), per (bin, cell) element, fp32).  Two roundings matter for the loss
+// record the stopping rule reads:
+//  * pi_jmax is fl(1 / s), s = the fp32 row sum of exp(z - max) with exp(0) = 1 for the argmax,
+//    so near saturation log pi_jmax moves in steps of ~2^-24 (and is 0 once s rounds to 1);
+//  * lgamma(sum eta) ~ 1.3e7 for the weight-1e6 priors (ulp 1): the element's value is rounded
+//    to that grid before any sum, and where thousands of elements' logits move in lockstep
+//    (late iterations) the reference's loss falls in steps of ~3.5e5 (tools/stop_probe.py).
+// The kernels add q = fl(xs + A) - A per element (A = the row's fp32 lgamma(sum eta), the eta
+// table's last column; 0 keeps xs unrounded) and the host the rows' fp32 lgamma(sum eta) -
+// sum lgamma(eta) (EtaCodebook.dirichlet_normaliser "torch32"): fl(fl(xs + A) - B) = q + (A - B)
+// exactly (both differences are exact: Sterbenz).
+
+// torch's CPU order for the fp32 sum of a contiguous row of P values (reduce over the last
+// dim; tests/test_dirichlet_value.py pins it): elements 8 .. P-1 first, then 0 .. 7, one
+// rounding per addition, for 9 <= P <= 15; 4 .. 0 .. 3 for P = 5; sequential otherwise (the
+// sequential order is exact for P <= 4 and P = 8, approximate for P = 6, 7, 16).
+template <int P>
+PERT_HD constexpr int torch_row_sum_index(int i) {
+  constexpr int split = (P >= 9 && P <= 15) ? 8 : (P == 5 ? 4 : 0);
+  return i < P - split ? split + i : i - (P - split);
+}
+
+// log of the reference's fp32 pi_jmax = exp(0) / s (SoftmaxTransform, transforms.py:951-954).
+template <int P>
+PERT_HD float ref_log_pi_jmax(const float (&z)[P], float zmax, int jmax) {
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const int k = torch_row_sum_index<P>(i);
+    s += (k == jmax) ? 1.0f : fexp(z[k] - zmax);
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float p = __fdiv_rn(1.0f, s);                  // IEEE division, as torch's probs / sum
+#else
+  const float p = 1.0f / s;
+#endif
+  const float d = 1.0f - p;                            // exact (p in [1/P, 1])
+  // log(1 - d): the series where p is near 1 (|error| < d^5 / 5 < 2e-10 d), the log elsewhere
+  return d < 0.015625f ? -d * (1.0f + d * (0.5f + d * (0.33333334f + 0.25f * d))) : flog(p);
+}
+
+// q = fl(xs + A) - A: xs rounded to the grid of the row's fp32 lgamma(sum eta) (A = 0: xs)
+PERT_HD float dir_site_round(float xs, float A) {
+  float t = xs + A;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(t));                          // keep the two roundings apart
+#endif
+  return t - A;
+}
+
 // pi_k from the EnumOnline summary (the exponential enum_online summed)
 template <int P>
 PERT_HD float enum_pi(const EnumOnline<P>& o, float zk, int k) {
@@ -726,9 +778,10 @@ PERT_HD float enum_tail(const EnumFwd<P>& o, const float (&z)[P], const float (&
                         float (&gz)[P]) {
   float dirv = 0.0f;
   float em[P + 1];
+  const float lpj = ref_log_pi_jmax<P>(z, o.zmax, o.jmax);
 #pragma unroll
   for (int k = 0; k < P; ++k) {
-    dirv += em1[k] * ((z[k] - o.zmax) - o.lse1p);
+    dirv += em1[k] * ((k == o.jmax) ? lpj : (z[k] - o.zmax) - o.lse1p);
     gz[k] = em1[k] - o.pi[k] * S1 + o.gcm[k] - o.pi[k] * o.sgm;
     em[k] = em1[k];
   }

@@ -96,10 +96,16 @@ class EtaCodebook:
         table[np.arange(P), np.arange(P)] = F32(weight)
         return cls(np.ascontiguousarray(s, dtype=np.uint16), table)
 
-    def kernel_table(self) -> np.ndarray:
-        """(n_codes, P+1): eta_k - 1, then S1 = sum_k (eta_k - 1) (include/pert_hip.h)."""
+    def kernel_table(self, round_site: bool = True) -> np.ndarray:
+        """(n_codes, P+2): eta_k - 1, then S1 = sum_k (eta_k - 1), then A = lgamma(sum eta)
+        in fp32 exactly as torch.distributions.Dirichlet.log_prob evaluates it (0 when
+        ``round_site`` is off): the kernels round each element's Dirichlet value to A's grid,
+        as the reference's fp32 value is rounded before it is summed (include/pert_hip.h,
+        pert_math.h dir_site_round; tests/test_dirichlet_value.py)."""
         em1 = self.table.astype(np.float64) - 1.0
-        out = np.concatenate([em1, em1.sum(1, keepdims=True)], axis=1)
+        t = torch.from_numpy(np.ascontiguousarray(self.table, dtype=F32))
+        A = torch.lgamma(t.sum(-1)).numpy() if round_site else np.zeros(len(em1), F32)
+        out = np.concatenate([em1, em1.sum(1, keepdims=True), A.astype(np.float64)[:, None]], axis=1)
         return out.astype(F32)
 
     def counts(self) -> np.ndarray:
@@ -348,7 +354,10 @@ class PertShard:
         else:
             self.eta_code = self._pad_rows(
                 torch.as_tensor(np.ascontiguousarray(eta.codes, dtype=np.uint16).view(np.int16)), dev)
-            self.eta_table = torch.as_tensor(eta.kernel_table(), device=dev).contiguous()
+            # the site value rounded as the reference's fp32 log_prob rounds it when the host
+            # adds the reference's fp32 normaliser ("torch32"), unrounded with the exact one
+            self.eta_table = torch.as_tensor(eta.kernel_table(round_site=(dirichlet_mode == "torch32")),
+                                             device=dev).contiguous()
             lam_f = float(np.asarray(lamb, dtype=F32).reshape(-1)[0])
             self.beta_means_t = torch.as_tensor(np.asarray(beta_means, dtype=F32).reshape(self.n_libs, self.K1),
                                                 device=dev).contiguous()
@@ -385,6 +394,8 @@ class PertShard:
 
         self.pass_events = None      # list -> (start, end) HIP events around every pass
         self.pass_event_stride = 1   # (one-rank loop) events around every stride-th iteration's pass
+        self._loop_bufs = None       # run_svi's control word / records / pinned host copy (reused)
+        self._ctl_init = None
 
         # ---- constants of the loss (added on the host, summed over ranks once)
         # (fp64 on the device, from the padded reads already there: zero columns add nothing; a
@@ -661,6 +672,28 @@ class PertShard:
             nat.check(self.lib.pert_adam(ctypes.byref(self._prob), ctypes.byref(self._state),
                                          ctypes.byref(self._hp), self._stream()), "pert_adam")
 
+    def _loop_buffers(self, n: int):
+        """The device loop's control word, its per-iteration loss records and their pinned host
+        copy, kept between fits of this shard (a pinned allocation costs far more than a step
+        of a small shard); grown to the next power of two when a fit needs more."""
+        cap = 0 if self._loop_bufs is None else self._loop_bufs[1].shape[0]
+        if n > cap:
+            cap = 1 << max(6, (n - 1).bit_length())
+            self._loop_bufs = (torch.empty(2, dtype=torch.int32, device=self.device),
+                               torch.empty((cap, 2), dtype=torch.float64, device=self.device),
+                               torch.empty((cap, 2), dtype=torch.float64, pin_memory=True))
+            self._ctl_init = torch.tensor([-1, 0], dtype=torch.int32, device=self.device)
+        return self._loop_bufs
+
+    def reserve_svi(self, n: int) -> None:
+        """Set up everything a run_svi(n) from the current step allocates or computes on the
+        host -- its loop buffers and, for step 1, the canonical pi trajectory -- ahead of the
+        call (run_pert_model computes the trajectory on its helper thread during the prep;
+        bench.py calls this before its timed region)."""
+        self._loop_buffers(int(n))
+        if self.pi_block is not None:
+            self.pi_block._cache(self.t + int(n) + 1)
+
     def run_svi(self, max_iter: int, min_iter: int, rel_tol: float, chunk: int = 8, depth: int = 8):
         """The SVI loop of pert_model.py:742-758 (:800-816, :867-883) without a per-step host
         synchronisation.  Every iteration's loss is recorded on the device and the reference's
@@ -677,9 +710,8 @@ class PertShard:
         if n <= 0:
             return [], 0
         dev = self.device
-        ctl = torch.tensor([-1, 0], dtype=torch.int32, device=dev)
-        rec = torch.zeros((n, 2), dtype=torch.float64, device=dev)
-        host = torch.empty((n, 2), dtype=torch.float64, pin_memory=True)
+        ctl, rec, host = self._loop_buffers(n)
+        ctl.copy_(self._ctl_init, non_blocking=True)
         offs = None
         t0 = self.t
         if self.pi_block is not None:
@@ -757,7 +789,7 @@ class PertShard:
             st.step = 0
         stop_at, reason = int(c[0]), int(c[1])
         n_done = stop_at + 1 if stop_at >= 0 else launched
-        losses = host[:n_done, 0].tolist()
+        losses = host[:n_done, 0].tolist()          # (copied out: the buffer is reused by the next fit)
         self.t = t0 + n_done
         if self.pi_block is not None and n_done > 0:
             self._pi_lp = self.pi_block.advance_to(t0 + n_done)

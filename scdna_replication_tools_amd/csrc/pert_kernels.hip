@@ -332,9 +332,9 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
       const float S1s = S1 + o.sgm;
       int jmax;
       float om;
-      enum_jmax<P>(zt, o, jmax, om);
+      float lpj;                                            // the reference's fp32 log pi_jmax
+      enum_jmax<P>(zt, o, jmax, om, lpj);
       const float tom = S1s * om;                           // (S1 + sgm)(1 - pi_jmax), jmax_grad
-      const float lpj = ref_log_pi_jmax<P>(zt, o.zmax, jmax);
       pf2 dirv2 = {0.0f, 0.0f};
       const float* mb = lds + 2 * SF;
       float* zo = st.z_pi + tile + lane;
@@ -347,8 +347,7 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
         const pf2 zz = {zt[k0], zt[k1]};
         const pf2 e1 = {em1[k0], k1 != k0 ? em1[k1] : 0.0f};
         const pf2 pk = pf2{enum_pi(o, zt[k0], k0), enum_pi(o, zt[k1], k1)};
-        const pf2 lp = (zz - o.zmax) - o.lse1p;
-        dirv2 += e1 * pf2{k0 == jmax ? lpj : lp.x, k1 == jmax ? lpj : lp.y};
+        dirv2 += e1 * ((zz - o.zmax) - o.lse1p);
         const pf2 gc = pf2{o.gcm[k0], o.gcm[k1]};
         pf2 gl = pk * S1s - e1 - gc;                                  // d(-ELBO)/dz
         const pf2 gj = ((S1 - e1) + (o.sgm - gc)) - tom;              // the argmax logit (jmax_grad)
@@ -375,7 +374,10 @@ __global__ void __launch_bounds__(64, 2) enum_dma_kernel(pert_problem pr, pert_s
           if constexpr (k1 != k0) gp[k1 * 64] = g1;
         }
       });
-      const float dirv = dir_site_round(dirv2.x + dirv2.y, Arow);
+      float wj = 0.0f;
+#pragma unroll
+      for (int k = 0; k < P; ++k) wj = (k == jmax) ? em1[k] : wj;
+      const float dirv = dir_site_round((dirv2.x + dirv2.y) + wj * (lpj + o.lse1p), Arow);
       if (valid) {
         loss += o.E + dirv;
         gtv = o.gt;
@@ -734,9 +736,9 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
         const float S1s = S1 + o.sgm;
         int jmax;
         float om;
-        enum_jmax<P>(z, o, jmax, om);
+        float lpj;                                          // the reference's fp32 log pi_jmax
+        enum_jmax<P>(z, o, jmax, om, lpj);
         const float tom = S1s * om;                         // (S1 + sgm)(1 - pi_jmax), jmax_grad
-        const float lpj = ref_log_pi_jmax<P>(z, o.zmax, jmax);   // the reference's fp32 log pi_jmax
         // planes in pairs, packed fp32 (the exponential, square root and reciprocal per element)
         pf2 dirv2 = {0.0f, 0.0f};
         pert_static_for<0, (P + 1) / 2>([&](auto pc) {
@@ -745,8 +747,7 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
           const pf2 zz = {z[k0], z[k1]};
           const pf2 e1 = {row[k0], k1 != k0 ? row[k1] : 0.0f};
           const pf2 pk = pf2{enum_pi(o, z[k0], k0), enum_pi(o, z[k1], k1)};
-          const pf2 lp = (zz - o.zmax) - o.lse1p;
-          dirv2 += e1 * pf2{k0 == jmax ? lpj : lp.x, k1 == jmax ? lpj : lp.y};
+          dirv2 += e1 * ((zz - o.zmax) - o.lse1p);
           const pf2 gc = pf2{o.gcm[k0], o.gcm[k1]};
           pf2 gl = pk * S1s - e1 - gc;                                  // d(-ELBO)/dz
           // the argmax logit: jmax_grad, evaluated at the plane that holds it
@@ -776,7 +777,9 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
               __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, g1), rg, voff, zoff + k1 * 256, 0);
           }
         });
-        dirv = dir_site_round(dirv2.x + dirv2.y, row[P + 1]);   // the site value's fp32 rounding
+        // the argmax plane's log pi as the reference's fp32 value (its term above used -lse1p),
+        // then the site value's fp32 rounding
+        dirv = dir_site_round((dirv2.x + dirv2.y) + row[jmax] * (lpj + o.lse1p), row[P + 1]);
       };
       if (etal) tail(s_tab + code * kTabRow(P));
       else tail(pr.eta_table + (size_t)code * kTabRow(P));

@@ -476,24 +476,6 @@ struct EnumOnline {
   int argmax;     // r * P + c of the joint MAP state (first maximum)
 };
 
-// The argmax logit (first maximum, as torch's max) and 1 - pi_jmax summed from the other
-// states (jmax_grad), from the logits and the EnumOnline summary -- evaluated where the
-// gradient is formed (the passes' tails), so neither is live through the NB chains.
-template <int P>
-PERT_HD void enum_jmax(const float (&z)[P], const EnumOnline<P>& o, int& jmax, float& om) {
-  float m = z[0];
-  jmax = 0;
-#pragma unroll
-  for (int k = 1; k < P; ++k) {
-    jmax = z[k] > m ? k : jmax;
-    m = fmaxf(m, z[k]);
-  }
-  float t = 0.0f;
-#pragma unroll
-  for (int k = 0; k < P; ++k) t += (k == jmax) ? 0.0f : fexp2(fmaf(z[k], kLog2e, -o.zmaxS));
-  om = t * o.inv1t;
-}
-
 // ---- the Dirichlet site's VALUE as the reference's fp32 arithmetic forms it
 // (torch.distributions.Dirichlet.log_prob: xlogy(eta - 1, pi).sum(-1) + lgamma(eta.sum(-1))
 //  - lgamma(eta).sum(-1), per (bin, cell) element, fp32).  Two roundings matter for the loss
@@ -518,7 +500,18 @@ PERT_HD constexpr int torch_row_sum_index(int i) {
   return i < P - split ? split + i : i - (P - split);
 }
 
-// log of the reference's fp32 pi_jmax = exp(0) / s (SoftmaxTransform, transforms.py:951-954).
+// log of the reference's fp32 pi_jmax = fl(exp(0) / s) (SoftmaxTransform, transforms.py:951-954)
+// from s, the row sum in torch's order.  The quotient by one Newton step on v_rcp (the FMA
+// residual makes it the correctly rounded 1 / s but for rare ties): near saturation pi moves in
+// steps of 2^-24 and W log pi in steps of ~0.06, which the site's grid of 1 resolves.
+PERT_HD float ref_log_pi_from_sum(float s) {
+  const float r = frcp(s);
+  const float p = fmaf(r, fmaf(-s, r, 1.0f), r);
+  const float d = 1.0f - p;                            // exact (p in [1/P, 1])
+  // log(1 - d): the series where p is near 1 (|error| < d^5 / 5 < 2e-10 d), the log elsewhere
+  return d < 0.015625f ? -d * (1.0f + d * (0.5f + d * (0.33333334f + 0.25f * d))) : flog(p);
+}
+
 template <int P>
 PERT_HD float ref_log_pi_jmax(const float (&z)[P], float zmax, int jmax) {
   float s = 0.0f;
@@ -527,14 +520,7 @@ PERT_HD float ref_log_pi_jmax(const float (&z)[P], float zmax, int jmax) {
     const int k = torch_row_sum_index<P>(i);
     s += (k == jmax) ? 1.0f : fexp(z[k] - zmax);
   }
-#if defined(__HIP_DEVICE_COMPILE__)
-  const float p = __fdiv_rn(1.0f, s);                  // IEEE division, as torch's probs / sum
-#else
-  const float p = 1.0f / s;
-#endif
-  const float d = 1.0f - p;                            // exact (p in [1/P, 1])
-  // log(1 - d): the series where p is near 1 (|error| < d^5 / 5 < 2e-10 d), the log elsewhere
-  return d < 0.015625f ? -d * (1.0f + d * (0.5f + d * (0.33333334f + 0.25f * d))) : flog(p);
+  return ref_log_pi_from_sum(s);
 }
 
 // q = fl(xs + A) - A: xs rounded to the grid of the row's fp32 lgamma(sum eta) (A = 0: xs)
@@ -544,6 +530,32 @@ PERT_HD float dir_site_round(float xs, float A) {
   asm volatile("" : "+v"(t));                          // keep the two roundings apart
 #endif
   return t - A;
+}
+
+// The argmax logit (first maximum, as torch's max) and 1 - pi_jmax summed from the other
+// states (jmax_grad), from the logits and the EnumOnline summary -- evaluated where the
+// gradient is formed (the passes' tails), so neither is live through the NB chains.
+// lpj: the reference's fp32 log pi_jmax (ref_log_pi_from_sum), from the same exponentials.
+template <int P>
+PERT_HD void enum_jmax(const float (&z)[P], const EnumOnline<P>& o, int& jmax, float& om, float& lpj) {
+  float m = z[0];
+  jmax = 0;
+#pragma unroll
+  for (int k = 1; k < P; ++k) {
+    jmax = z[k] > m ? k : jmax;
+    m = fmaxf(m, z[k]);
+  }
+  // (the argmax's exponential is fexp(0) = 1 exactly, as torch's exp(0))
+  float t = 0.0f, s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const int k = torch_row_sum_index<P>(i);
+    const float e = fexp(z[k] - o.zmax);
+    t += (k == jmax) ? 0.0f : e;
+    s += e;
+  }
+  om = t * o.inv1t;
+  lpj = ref_log_pi_from_sum(s);
 }
 
 // pi_k from the EnumOnline summary (the exponential enum_online summed)

@@ -1,13 +1,26 @@
 #!/bin/bash
-# A/B the enumerated pass across libpert_hip builds on one box (interleaved, 2 rounds).
-#   tools/ab_bench.sh "libA.so libB.so ..." [bench args]
+# Interleaved A/B of the default build against another build of the same ABI (PERT_LIB), three
+# rounds on one box: C4 step 2, the 1,250-cell shard and C5.
+# usage: tools/ab_bench.sh TAG LIB.so
 set -o pipefail
-LIBS=$1; shift
-ARGS=${*:-"--no-cpu-baseline"}
+TAG=${1:-ab}; LIB=$2
 mkdir -p gpurun_out
-for round in 1 2; do
-  for L in $LIBS; do
-    PERT_LIB=$(pwd)/scdna_replication_tools_amd/$L timeout -k 10 200 python bench.py $ARGS > gpurun_out/ab_${L}_$round.log 2>&1 || exit 1
-    echo "$round $L $(tail -1 gpurun_out/ab_${L}_$round.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("step_ms", round(d["ms_per_step"],4), "kernel_ms", round(d["roofline"]["kernel_ms"],4))')"
-  done
+OUT=gpurun_out/${TAG}_ab.log
+: > $OUT
+row() {
+  local label=$1; shift
+  timeout -k 10 150 python bench.py --steps 30 --warmup 3 --no-cpu-baseline "$@" > gpurun_out/${TAG}_ab.tmp 2>&1 || { tail -5 gpurun_out/${TAG}_ab.tmp; exit 1; }
+  python -c "
+import json
+r = json.loads(open('gpurun_out/${TAG}_ab.tmp').read().strip().splitlines()[-1]); rf = r['roofline']
+print('$label', r['config']['config'], 'cells', r['config']['cells'], 'step_ms', round(r['ms_per_step'], 4), 'pass_ms', round(rf['kernel_ms'], 4), 'ceiling_ms', round(rf.get('pattern_ceiling', {}).get('ms', 0), 4))
+" | tee -a $OUT
+}
+for rep in 1 2 3; do
+  row new || exit 1
+  PERT_LIB=$PWD/$LIB row old || exit 1
+  row new --cells 1250 || exit 1
+  PERT_LIB=$PWD/$LIB row old --cells 1250 || exit 1
 done
+row new --config c5 || exit 1
+PERT_LIB=$PWD/$LIB row old --config c5 || exit 1

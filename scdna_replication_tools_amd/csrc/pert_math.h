@@ -501,15 +501,14 @@ PERT_HD constexpr int torch_row_sum_index(int i) {
 }
 
 // log of the reference's fp32 pi_jmax = fl(exp(0) / s) (SoftmaxTransform, transforms.py:951-954)
-// from s, the row sum in torch's order.  The quotient by one Newton step on v_rcp (the FMA
-// residual makes it the correctly rounded 1 / s but for rare ties): near saturation pi moves in
-// steps of 2^-24 and W log pi in steps of ~0.06, which the site's grid of 1 resolves.
+// from s, the row sum in torch's order.  Where the rounding of pi matters -- the saturated
+// elements, whose logits move in lockstep -- s = 1 + ds with ds a few 2^-23 and fl(1 / s) is
+// exactly 1 - ds (for ds < 2^-13 the ds^2 term is below half an ulp of 1 - ds), so
+// log pi = log(1 - ds) by its series (|error| < ds^5 / 5); above, -log(s), which differs from
+// log(fl(1 / s)) by the quotient's rounding only (<= 2^-24 relative, no lockstep there).
 PERT_HD float ref_log_pi_from_sum(float s) {
-  const float r = frcp(s);
-  const float p = fmaf(r, fmaf(-s, r, 1.0f), r);
-  const float d = 1.0f - p;                            // exact (p in [1/P, 1])
-  // log(1 - d): the series where p is near 1 (|error| < d^5 / 5 < 2e-10 d), the log elsewhere
-  return d < 0.015625f ? -d * (1.0f + d * (0.5f + d * (0.33333334f + 0.25f * d))) : flog(p);
+  const float ds = s - 1.0f;                           // exact (s in [1, P])
+  return ds < 1.220703125e-4f ? -ds * (1.0f + ds * (0.5f + ds * (0.33333334f + 0.25f * ds))) : -flog(s);
 }
 
 template <int P>
@@ -545,14 +544,15 @@ PERT_HD void enum_jmax(const float (&z)[P], const EnumOnline<P>& o, int& jmax, f
     jmax = z[k] > m ? k : jmax;
     m = fmaxf(m, z[k]);
   }
-  // (the argmax's exponential is fexp(0) = 1 exactly, as torch's exp(0))
+  // (the exponentials are enum_pi's, shared with the tail's pi_k; the argmax adds exactly 1,
+  // torch's exp(0))
   float t = 0.0f, s = 0.0f;
 #pragma unroll
   for (int i = 0; i < P; ++i) {
     const int k = torch_row_sum_index<P>(i);
-    const float e = fexp(z[k] - o.zmax);
+    const float e = fexp2(fmaf(z[k], kLog2e, -o.zmaxS));
     t += (k == jmax) ? 0.0f : e;
-    s += e;
+    s += (k == jmax) ? 1.0f : e;
   }
   om = t * o.inv1t;
   lpj = ref_log_pi_from_sum(s);

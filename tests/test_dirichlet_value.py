@@ -76,17 +76,20 @@ def test_dirichlet_xlogy_value_matches_torch_fp32(nat):
     # where the rounding of pi_jmax matters: pi32_jmax itself is torch's (the value moves in
     # steps of W 2^-24 ~ 0.06 there), its log within 2 ulp (torch's vectorised logf and the
     # kernels' series differ in the last bit at ties; 1e-8 against the site's grid of 1)
-    sat = 1.0 - pi.numpy()[np.arange(n), st] < 1e-3
+    om = 1.0 - pi.numpy()[np.arange(n), st]
+    sat = om < 1e-4                                          # s - 1 < 2^-13: fl(1 / s) = 2 - s
     assert sat.sum() > 500 and (err[sat] <= 2).mean() > 0.999, err[sat].max()
-    # elsewhere exp / log of other libms: a few ulp
-    assert (err <= 8).mean() > 0.999, err.max()
+    # above, -log(s): off by the quotient's rounding, at most W 2^-24 (no lockstep there)
+    # everywhere: the quotient's rounding (W 2^-24) and a few ulp of other libms' exp / log
+    assert (np.abs(got - ref) <= float(W) * 2.0 ** -24 + 8 * ulp).mean() > 0.999
     # and the rounded site value: fl(fl(xs + A) - B) = (fl(xs + A) - A) + (A - B)
     eta = torch.tensor(em1 + 1.0)
     A = torch.lgamma(eta.sum(-1)).numpy()
     B = torch.lgamma(eta).sum(-1).numpy()
     site = (torch.tensor(ref) + torch.tensor(A) - torch.tensor(B)).numpy()   # torch's own order
     q = ((got + A).astype(np.float32) - A).astype(np.float32)
-    assert (q.astype(np.float64) + (A.astype(np.float64) - B) == site).mean() > 0.999
+    same = q.astype(np.float64) + (A.astype(np.float64) - B) == site
+    assert same[sat].mean() > 0.999 and same.mean() > 0.99, (same[sat].mean(), same.mean())
 
 
 def test_kernel_table_rounding_column():

@@ -99,6 +99,12 @@ typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 #ifndef PERT_NT_STORE
 #define PERT_NT_STORE 1
 #endif
+// cache policy of enum3's streamed z / m / v (g) stores (gfx950 CPol bits: 1 sc0, 2 nt, 16 sc1);
+// A/B knob: 2 = nt (default), 19 = sc0 sc1 nt (written through: no dirty L2 lines left for the
+// end-of-kernel release)
+#ifndef PERT_STORE_CPOL
+#define PERT_STORE_CPOL 2
+#endif
 __device__ __forceinline__ void store_stream(float* p, float v) {
 #if PERT_NT_STORE
   __builtin_nontemporal_store(v, p);
@@ -549,7 +555,7 @@ __device__ __forceinline__ unsigned int arrive(unsigned int* c, unsigned int v) 
 template <int K>
 __device__ __forceinline__ void store_nt(__amdgpu_buffer_rsrc_t rs, float v, uint32_t voff, uint32_t soff) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs, voff, soff + K * 256,
-                                        PERT_NT_STORE ? 2 : 0);
+                                        PERT_NT_STORE ? PERT_STORE_CPOL : 0);
 }
 
 template <int K1T>

@@ -544,8 +544,9 @@ PERT_HD void enum_jmax(const float (&z)[P], const EnumOnline<P>& o, int& jmax, f
     jmax = z[k] > m ? k : jmax;
     m = fmaxf(m, z[k]);
   }
-  // (the exponentials are enum_pi's, shared with the tail's pi_k; the argmax adds exactly 1,
-  // torch's exp(0))
+  // the exponentials are enum_pi's (shared with the tail's pi_k): 2^(z_k log2e - fl(m log2e)),
+  // i.e. torch's exp(z_k - m) scaled by c = 2^d, d = m log2e - fl(m log2e) (|d| < 2^-20); the
+  // argmax adds exactly 1 to the row sum, as torch's exp(0)
   float t = 0.0f, s = 0.0f;
 #pragma unroll
   for (int i = 0; i < P; ++i) {
@@ -554,7 +555,9 @@ PERT_HD void enum_jmax(const float (&z)[P], const EnumOnline<P>& o, int& jmax, f
     t += (k == jmax) ? 0.0f : e;
     s += (k == jmax) ? 1.0f : e;
   }
-  om = t * o.inv1t;
+  // 1 - pi_jmax from exp(z_k - m) themselves: t / c, to first order in d
+  const float d = fmaf(m, kLog2e, -o.zmaxS);
+  om = (t * o.inv1t) * fmaf(-d, kLn2, 1.0f);
   lpj = ref_log_pi_from_sum(s);
 }
 

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Build libpert_hip from THIS tree's kernel sources with extra compile flags (A/B knobs):
+#   tools/build_variant.sh OUT.so -DKNOB=VALUE ...   then   PERT_LIB=OUT.so python bench.py ...
+set -euo pipefail
+OUT=$1; shift
+R=$(pwd)
+T=$(mktemp -d)
+HIPCC="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-slp-vectorize -fno-signed-zeros"
+$HIPCC "$@" -I $R/include -c $R/scdna_replication_tools_amd/csrc/pert_kernels.hip -o $T/k.o
+$HIPCC -I $R/include -c $R/scdna_replication_tools_amd/csrc/tau_kernels.hip -o $T/tau.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $T/k.o $T/tau.o -o $OUT
+rm -rf $T

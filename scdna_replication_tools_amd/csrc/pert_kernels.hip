@@ -998,7 +998,8 @@ __global__ void __launch_bounds__(kBlock) obs_kernel(pert_problem pr, pert_state
 // waves waiting on their own chain 63 % of the time (profiles/r03b_s1).  One wave per
 // workgroup, no barrier in the bin loop; per-bin rho sums by a wave reduction, staged in LDS
 // and stored once per tile.
-constexpr int kMaxLTObs = 128;
+constexpr int kMaxLTObs = 512;       // the pair pass's LDS (per-bin constants) is sized by its tile
+constexpr int kPlanMaxLTObs = 128;   // longest tile the step-1 planner considers
 
 template <int K1T>
 __global__ void __launch_bounds__(64) obs_pair_kernel(pert_problem pr, pert_state st) {
@@ -1013,8 +1014,11 @@ __global__ void __launch_bounds__(64) obs_pair_kernel(pert_problem pr, pert_stat
   const int l1 = min(pr.L, l0 + LT);
   const pert_layout lay = st.lay;
 
-  __shared__ float s_bc[kMaxLTObs * (K1T + 1)];
-  __shared__ float s_bin[kMaxLTObs];
+  // dynamic LDS (obs_pair_lds_bytes): per bin of the tile rho and the GC features, then the
+  // per-bin rho sums
+  extern __shared__ float obs_lds[];
+  float* s_bc = obs_lds;
+  float* s_bin = obs_lds + (size_t)st.bins_per_tile * (K1T + 1);
   // per-bin constants of the tile (constrained rho, GC features), requested first
   for (int i = lane; i < (l1 - l0) * (K1 + 1); i += 64) {
     const int lb = i / (K1 + 1), j = i - lb * (K1 + 1);
@@ -2200,17 +2204,20 @@ int pert_auto_bins_per_tile(const pert_problem* prob, int32_t variant, int32_t* 
     // reads) 2 (K1 + 1) partial floats per pair, against 5 B per pair and bin of input, so
     // longer tiles cut traffic; but the launch takes ceil(tiles / slots) rounds and a last
     // round that fills few slots idles most of the chip.  Least (rounds + 1/8) x (lt + 8),
-    // the 8 being the partials' cost in bins, over lt in [32, kMaxLTObs].
+    // the 8 being the partials' cost in bins, over lt in [32, kPlanMaxLTObs].
     int nb = 0;
+    const int K1T = prob->K1 == 5 ? 5 : PERT_MAX_K1;
     if (prob->K1 == 5)
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, obs_pair_kernel<5>, 64, 0);
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, obs_pair_kernel<5>, 64,
+                                                       obs_pair_lds_bytes(K1T, kPlanMaxLTObs));
     else
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, obs_pair_kernel<PERT_MAX_K1>, 64, 0);
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, obs_pair_kernel<PERT_MAX_K1>, 64,
+                                                       obs_pair_lds_bytes(K1T, kPlanMaxLTObs));
     if (e != hipSuccess) return hip_status(e);
     const long slots = (long)ncu * (nb > 0 ? nb : 16);
     const long n_ct = obs_cell_tiles(prob);
     long best = -1;
-    for (int lt = kMaxLTObs; lt >= 32; --lt) {
+    for (int lt = kPlanMaxLTObs; lt >= 32; --lt) {
       const long tiles = n_ct * ((prob->L + lt - 1) / lt);
       const long rounds = (tiles + slots - 1) / slots;
       const long cost = (8 * rounds + 1) * (lt + 8);
@@ -2311,6 +2318,8 @@ int pert_adam_shared(const pert_problem* prob, pert_state* st, const pert_adam_h
   return hip_status(hipGetLastError());
 }
 
+size_t obs_pair_lds_bytes(int K1T, int lt) { return sizeof(float) * (size_t)lt * (K1T + 2); }
+
 int pert_obs_pass(const pert_problem* prob, pert_state* st, hipStream_t stream) {
   if (!problem_ok(prob) || !st || prob->kind != PERT_KIND_STEP1) return PERT_E_ARG;
   if (!prob->cn_obs || !st->cell_part || !st->bin_part || !st->blk_part) return PERT_E_ARG;
@@ -2320,9 +2329,10 @@ int pert_obs_pass(const pert_problem* prob, pert_state* st, hipStream_t stream) 
   if (!pair_mode(prob))
     hipLaunchKernelGGL(obs_kernel, grid, dim3(kBlock), 0, stream, *prob, s2);
   else if (prob->K1 == 5)
-    hipLaunchKernelGGL(obs_pair_kernel<5>, grid, dim3(64), 0, stream, *prob, s2);
+    hipLaunchKernelGGL(obs_pair_kernel<5>, grid, dim3(64), obs_pair_lds_bytes(5, s2.bins_per_tile), stream, *prob, s2);
   else
-    hipLaunchKernelGGL(obs_pair_kernel<PERT_MAX_K1>, grid, dim3(64), 0, stream, *prob, s2);
+    hipLaunchKernelGGL(obs_pair_kernel<PERT_MAX_K1>, grid, dim3(64),
+                       obs_pair_lds_bytes(PERT_MAX_K1, s2.bins_per_tile), stream, *prob, s2);
   return hip_status(hipGetLastError());
 }
 

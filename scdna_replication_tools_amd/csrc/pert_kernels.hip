@@ -1000,6 +1000,7 @@ __global__ void __launch_bounds__(kBlock) obs_kernel(pert_problem pr, pert_state
 // and stored once per tile.
 constexpr int kMaxLTObs = 512;       // the pair pass's LDS (per-bin constants) is sized by its tile
 constexpr int kPlanMaxLTObs = 128;   // longest tile the step-1 planner considers
+inline size_t obs_pair_lds_bytes(int K1T, int lt) { return sizeof(float) * (size_t)lt * (K1T + 2); }
 
 template <int K1T>
 __global__ void __launch_bounds__(64) obs_pair_kernel(pert_problem pr, pert_state st) {
@@ -2317,8 +2318,6 @@ int pert_adam_shared(const pert_problem* prob, pert_state* st, const pert_adam_h
   hipLaunchKernelGGL(adam_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, *prob, *st, *hp, n);
   return hip_status(hipGetLastError());
 }
-
-size_t obs_pair_lds_bytes(int K1T, int lt) { return sizeof(float) * (size_t)lt * (K1T + 2); }
 
 int pert_obs_pass(const pert_problem* prob, pert_state* st, hipStream_t stream) {
   if (!problem_ok(prob) || !st || prob->kind != PERT_KIND_STEP1) return PERT_E_ARG;

@@ -1454,11 +1454,19 @@ __device__ void fin_global(const pert_problem& pr, const pert_state& st, int n_b
   const int lane = tid & 63, wave = tid >> 6;
   // (1) the observed pass's workgroup partials (step 1; none for the enumerated passes):
   //     all 1024 threads, double4 per workgroup, one LDS round
+  //     (kGU partials per thread in flight per round trip: clamped index, masked value; the
+  //     same per-thread order as one at a time)
+  constexpr int kGU = 8;
   double v[kBlkSlots] = {0.0, 0.0, 0.0, 0.0};
   const double4* bp4 = reinterpret_cast<const double4*>(st.blk_part);
-  for (int b = tid; b < n_blk; b += kFinBlock) {
-    const double4 q = bp4[b];
-    v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+  for (int b0 = tid; b0 < n_blk; b0 += kFinBlock * kGU) {
+    double4 q[kGU];
+#pragma unroll
+    for (int u = 0; u < kGU; ++u) q[u] = bp4[min(b0 + u * kFinBlock, n_blk - 1)];
+#pragma unroll
+    for (int u = 0; u < kGU; ++u) {
+      if (b0 + u * kFinBlock < n_blk) { v[0] += q[u].x; v[1] += q[u].y; v[2] += q[u].z; v[3] += q[u].w; }
+    }
   }
 #pragma unroll
   for (int j = 0; j < kBlkSlots; ++j) v[j] = wave_sum_d(v[j]);
@@ -1472,7 +1480,14 @@ __device__ void fin_global(const pert_problem& pr, const pert_state& st, int n_b
   const int nlk = nl * K1;
   for (int sl = wave; sl < nslot; sl += kSW) {
     double acc = 0.0;
-    for (int b = lane; b < n_cblk; b += 64) acc += st.cellblk_part[(size_t)b * nslot + sl];
+    for (int b0 = lane; b0 < n_cblk; b0 += 64 * kGU) {
+      double q[kGU];
+#pragma unroll
+      for (int u = 0; u < kGU; ++u) q[u] = st.cellblk_part[(size_t)min(b0 + 64 * u, n_cblk - 1) * nslot + sl];
+#pragma unroll
+      for (int u = 0; u < kGU; ++u)
+        if (b0 + 64 * u < n_cblk) acc += q[u];
+    }
     acc = wave_sum_d(acc);
     if (lane == 0) {
       if (sl < nlk) {
@@ -2240,13 +2255,15 @@ int pert_auto_bins_per_tile(const pert_problem* prob, int32_t variant, int32_t* 
     // cell-tile x bin-tile sweep of profiles/r02q, r02r).  A shard small enough that ONE
     // round of longer tiles leaves some slots free (1,250 cells, the per-rank shard of an
     // 8-GPU run) does better that way (0.87 vs 0.86 at 12 bins): each wave pays one tile
-    // prologue and the round has no tail of late tiles.  Take the shortest such tile
-    // from 36 bins up, else 12.
+    // prologue and the round has no tail of late tiles.  Take the shortest such tile from 36
+    // bins up that leaves a third of the slots free, else 12 (1,250 cells: 54 bins, 2,020
+    // tiles, 1.0-1.7 % shorter steps than 42 bins / 85 % of the slots in two interleaved
+    // leases, profiles/r04f_lt_ab.log, r04n_sweep.log).
     const int occ = step_occupancy(*prob, kShortLT3, 3);
     const long slots = (long)ncu * (occ > 0 ? occ : 8);
     for (int lt = 36; lt <= kMaxLT; ++lt) {
       const long tiles = n_ct * ((prob->L + lt - 1) / lt);
-      if (20 * tiles <= 17 * slots) {
+      if (3 * tiles <= 2 * slots) {
         *out = lt;
         return PERT_OK;
       }

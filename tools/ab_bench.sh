@@ -13,7 +13,7 @@ row() {
   python -c "
 import json
 r = json.loads(open('gpurun_out/${TAG}_ab.tmp').read().strip().splitlines()[-1]); rf = r['roofline']
-print('$label', r['config']['config'], 'cells', r['config']['cells'], 'step_ms', round(r['ms_per_step'], 4), 'pass_ms', round(rf['kernel_ms'], 4), 'ceiling_ms', round(rf.get('pattern_ceiling', {}).get('ms', 0), 4))
+print('$label', r['config']['config'], r['config']['fit'], 'cells', r['config']['cells'], 'LT', r['config']['bins_per_tile'], 'step_ms', round(r['ms_per_step'], 4), 'pass_ms', round(rf['kernel_ms'], 4), 'ceiling_ms', round((rf.get('pattern_ceiling') or {}).get('ms', 0), 4))
 " | tee -a $OUT
 }
 for rep in 1 2 3; do
@@ -21,6 +21,8 @@ for rep in 1 2 3; do
   PERT_LIB=$PWD/$LIB row old || exit 1
   row new --cells 1250 || exit 1
   PERT_LIB=$PWD/$LIB row old --cells 1250 || exit 1
+  row new --fit step1 || exit 1
+  PERT_LIB=$PWD/$LIB row old --fit step1 || exit 1
 done
 row new --config c5 || exit 1
 PERT_LIB=$PWD/$LIB row old --config c5 || exit 1

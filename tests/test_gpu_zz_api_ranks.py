@@ -40,7 +40,7 @@ def _fit(**extra):
 def _api_worker(rank, world, port, out_dir):
     import faulthandler
     import sys
-    faulthandler.dump_traceback_later(170, exit=True, file=sys.stderr)   # a hung rank shows where
+    faulthandler.dump_traceback_later(120, exit=True, file=sys.stderr)   # a hung rank shows where
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{}".format(port), rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)

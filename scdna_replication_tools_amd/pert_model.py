@@ -378,11 +378,23 @@ class pert_infer_scRT():
             out[k] = v[sl] if k in ("expose_tau", "expose_u", "expose_betas") else v
         return out
 
+    # one-launch steps (pert_enum_step: pass, reductions, priors, Adam and the loss record in
+    # one launch) where launch latency, not the pass, sets the step time: one rank and at most
+    # this many cell.bins (the C1 stand-in, 400 cells x 271 bins); PERT_FUSED=0/1 forces it
+    FUSED_MAX_CELLBINS = 1 << 21
+
+    def _fused(self, kind, dd: "_Dist", n_cellbins: int) -> bool:
+        mode = os.environ.get("PERT_FUSED", "auto")
+        if mode in ("0", "1"):
+            return mode == "1" and dd.world == 1
+        return dd.world == 1 and kind != KIND_STEP1 and n_cellbins <= self.FUSED_MAX_CELLBINS
+
     def _shard(self, kind, dd: _Dist, reads, libs, init, eta=None, **kw):
         """PertShard over this rank's contiguous cell range of the fit."""
         N = reads.shape[1]
         s0, s1 = dd.bounds(N)
         sl = slice(s0, s1)
+        kw.setdefault("fused", self._fused(kind, dd, reads.shape[0] * (s1 - s0)))
         if eta is not None:
             eta = eta.cells(sl)
         for k in ("cn_obs", "rep_obs"):

@@ -2259,14 +2259,26 @@ int pert_auto_bins_per_tile(const pert_problem* prob, int32_t variant, int32_t* 
     // bins up that leaves a third of the slots free, else 12 (1,250 cells: 54 bins, 2,020
     // tiles, 1.0-1.7 % shorter steps than 42 bins / 85 % of the slots in two interleaved
     // leases, profiles/r04f_lt_ab.log, r04n_sweep.log).
+    // A shard far smaller still (a few cell tiles: the C1 stand-in, the 64-cell genome-length
+    // chain) leaves the chip idle at any tile length, and a lone wave's bin costs ~6 us of
+    // latency (profiles/r04s: 209 us for 36-bin tiles of 400 cells x 271 bins), so shorter
+    // tiles win until the partial rows the reductions read over the bin tiles (64 per round
+    // trip, ~2 us each) catch up: least 6 (lt + 2) + 2 ceil(n_bt / 64) over the tile lengths
+    // from 4 bins up that fit, the longer tile on a tie.
     const int occ = step_occupancy(*prob, kShortLT3, 3);
     const long slots = (long)ncu * (occ > 0 ? occ : 8);
-    for (int lt = 36; lt <= kMaxLT; ++lt) {
-      const long tiles = n_ct * ((prob->L + lt - 1) / lt);
-      if (3 * tiles <= 2 * slots) {
-        *out = lt;
-        return PERT_OK;
-      }
+    long best_cost = -1;
+    int best = 0;
+    for (int lt = 4; lt <= kMaxLT; ++lt) {
+      const long n_bt = (prob->L + lt - 1) / lt;
+      const long tiles = n_ct * n_bt;
+      if (3 * tiles > 2 * slots) continue;
+      const long cost = 6 * (lt + 2) + 2 * ((n_bt + 63) / 64);
+      if (best_cost < 0 || cost <= best_cost) { best_cost = cost; best = lt; }
+    }
+    if (best > 0) {
+      *out = best;
+      return PERT_OK;
     }
     // many rounds (10 k cells: 15 rounds at 18 bins) -> 18 bins: the same kernel as 12 and a
     // third fewer per-cell partials for finalize (step -1 %, profiles/r02u); fewer -> 12

@@ -482,8 +482,14 @@ def main():
                     rec["roofline"]["traffic"] = pn["hbm_bytes_per_launch"]
                     rec["roofline"]["traffic_per_algorithmic"] = pn["hbm_bytes_per_launch"] / (bpc * local_cb)
                 p = pn["pmc"]
-                if p.get("SQ_ACTIVE_INST_ANY"):
-                    rec["roofline"]["wait_inst_frac"] = p.get("SQ_WAIT_INST_ANY", 0.0) / p["SQ_ACTIVE_INST_ANY"]
+                if p.get("SQ_WAVE_CYCLES"):
+                    # where the pass's wave-cycles go (the three counters partition them): issuing,
+                    # waiting on an instruction dependency / issue slot, waiting on memory (s_waitcnt)
+                    wc = p["SQ_WAVE_CYCLES"]
+                    rec["roofline"]["wave_cycles"] = {
+                        "active_inst": p.get("SQ_ACTIVE_INST_ANY", 0.0) / wc,
+                        "wait_inst": p.get("SQ_WAIT_INST_ANY", 0.0) / wc,
+                        "wait_mem": p.get("SQ_WAIT_ANY", 0.0) / wc}
         if world == 1 and not args.no_cpu_baseline and args.fit == "step2" and args.prior == "g1_clones":
             data = synth(max(args.cpu_cells, 3), subdiv, seed=0, device=device)
             rec["cpu_baseline"] = cpu_baseline(data, args.cpu_cells, args.cpu_steps)

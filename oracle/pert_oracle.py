@@ -432,8 +432,13 @@ def _chunked_backward(prob: OracleProblem, params, cell_chunk: int, ploidy) -> f
 
 
 # --------------------------------------------------------------------------- decode
-def enum_scores(prob: OracleProblem, z: Dict[str, torch.Tensor]) -> torch.Tensor:
-    """(2, P, L, N) joint log score of (rep, cn) at the point z (steps 2/3)."""
+def enum_score_terms(prob: OracleProblem, z: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    """The (2, P, L, N) joint log score of (rep, cn) at the point z (steps 2/3) and its
+    parts: ``lp_cn`` (P, L, N), ``lp_rep`` (2, 1, L, N), ``lp_reads`` (2, P, L, N), the
+    parameter-free part of the reads term ``kappa`` (L, N: x log lam + x log x - x -
+    lgamma(1 + x), the same for every state), ``delta`` and ``dpsi`` = d lp_reads / d delta
+    (2, P, L, N; 0 where delta is clamped) -- the magnitudes an fp32 evaluation's rounding
+    scales with (tests/_bounds.decode_mismatches)."""
     c = constrain(prob.kind, z)
     x = prob.reads
     L, N = x.shape
@@ -453,9 +458,22 @@ def enum_scores(prob: OracleProblem, z: Dict[str, torch.Tensor]) -> torch.Tensor
     rep = torch.tensor([0., 1.], dtype=dt).reshape(2, 1, 1, 1)
     chi = cn * (1. + rep)
     delta = u * chi * omega * (1 - lamb) / lamb
-    delta = torch.where(delta < 1, torch.ones_like(delta), delta)
-    return (Categorical(pi).log_prob(cn) + Bernoulli(phi).log_prob(rep)
-            + NegativeBinomial(delta, probs=lamb).log_prob(x))
+    clamped = delta < 1
+    delta = torch.where(clamped, torch.ones_like(delta), delta)
+    lp_cn = Categorical(pi).log_prob(cn)
+    lp_rep = Bernoulli(phi).log_prob(rep)
+    lp_reads = NegativeBinomial(delta, probs=lamb).log_prob(x)
+    xlx = torch.where(x > 0, x * torch.log(torch.where(x > 0, x, torch.ones_like(x))), torch.zeros_like(x))
+    kappa = x * torch.log(lamb) + xlx - x - torch.lgamma(1 + x)
+    dpsi = torch.where(clamped, torch.zeros_like(delta),
+                       torch.log1p(-lamb) + torch.digamma(delta + x) - torch.digamma(delta))
+    return dict(score=lp_cn + lp_rep + lp_reads, lp_cn=lp_cn, lp_rep=lp_rep, lp_reads=lp_reads, kappa=kappa,
+                delta=delta, dpsi=dpsi)
+
+
+def enum_scores(prob: OracleProblem, z: Dict[str, torch.Tensor]) -> torch.Tensor:
+    """(2, P, L, N) joint log score of (rep, cn) at the point z (steps 2/3)."""
+    return enum_score_terms(prob, z)["score"]
 
 
 @torch.no_grad()

@@ -952,16 +952,20 @@ def build_cn_prior(states, weight: float, P: int) -> EtaCodebook:
 
 
 def build_clone_cn_prior(cn: pd.DataFrame, cells, loci_chr, loci_start, profiles: pd.DataFrame, weight: float,
-                         P: int, cell_col="cell_id", clone_col="clone_id", keys=None) -> EtaCodebook:
+                         P: int, cell_col="cell_id", clone_col="clone_id", keys=None,
+                         cell_range: slice = None) -> EtaCodebook:
     """pert_model.py:285-296: the consensus clone profile (int64-truncated) as prior state --
     truncated and range-checked per clone, then one uint16 gather of the clone columns
-    (the same codes as build_cn_prior on the (L, N) profile matrix)."""
+    (the same codes as build_cn_prior on the (L, N) profile matrix).  ``cell_range``: the
+    code book of that contiguous range of ``cells`` only (a rank's shard)."""
     clones = first_clone(cn, cells, cell_col, clone_col, keys)
     mat, ci = _profile_columns(profiles, clones, loci_chr, loci_start)
     st = mat.astype(np.int64)
-    used = st[:, np.unique(ci)]
+    used = st[:, np.unique(ci)]          # every cell's clone: each rank of a sharded fit raises alike
     if used.size and (used.min() < 0 or used.max() >= P):      # before the uint16 narrowing
         raise ValueError("CN states must lie in [0, P) for P={}".format(P))
+    if cell_range is not None:
+        ci = ci[cell_range]
     return EtaCodebook.from_states(np.take(st.astype(np.uint16), ci, axis=1), weight, P)
 
 

@@ -37,6 +37,7 @@ exact path against sklearn and the whole against prep.guess_times, up to 5,451 b
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import threading
 import time
@@ -79,6 +80,50 @@ def _private_lloyd():
 _lloyd_unwrapped = _private_lloyd()
 # the public fallback enters threadpoolctl on every call: one caller at a time
 _KMEANS_LOCK = threading.Lock()
+
+
+def _sklearn_threadpool_controller():
+    """sklearn's process-wide threadpoolctl controller (utils/parallel.py
+    ``_get_threadpool_controller``, created by its first caller), or None."""
+    try:
+        from sklearn.utils.parallel import _get_threadpool_controller
+    except ImportError:
+        return None
+    return _get_threadpool_controller()
+
+
+def prepare_host_threads():
+    """Make, on the calling thread, every scan of the process's loaded libraries that the
+    tau initialiser would otherwise make later from a helper thread; returns sklearn's
+    controller (or None).
+
+    threadpoolctl finds the BLAS / OpenMP libraries with ``dl_iterate_phdr`` and a ctypes
+    Python callback: the dynamic loader's lock is held while the callback waits for the
+    GIL.  A thread that holds the GIL and loads a library at that moment -- an extension
+    module import, or a ``ctypes.PyDLL`` call (libpert_hip's launch entry points) whose
+    HIP runtime call dlopens -- waits for the loader's lock, and neither thread moves
+    again (tools/dl_deadlock_repro.py reproduces it on the CPU within seconds).  The two
+    scans are ``_HostHelper``'s search for numpy's BLAS and the creation of sklearn's
+    controller (the GaussianMixture / KMeans fallback paths); both are made once per
+    process, so after this call no thread of a fit makes one."""
+    _HostHelper.get()
+    return _sklearn_threadpool_controller()
+
+
+@contextlib.contextmanager
+def host_threads():
+    """The fit's host-thread discipline, entered on the fit thread before its helper thread
+    starts and left after the helper has ended: the library scans made now
+    (``prepare_host_threads``) and, when the public KMeans fallback is in use, the BLAS
+    libraries held at one thread for the whole fit -- sklearn's per-call limit then sets
+    the thread count to the value it already has instead of raising OpenBLAS's pool again
+    while another thread of the fit is inside a BLAS call."""
+    ctl = prepare_host_threads()
+    if _lloyd_unwrapped is None and ctl is not None:
+        with ctl.limit(limits=1, user_api="blas"):
+            yield
+    else:
+        yield
 
 
 def _tolerance(X: np.ndarray, tol: float) -> float:
@@ -806,6 +851,10 @@ def exact_fractions(norm_cols: np.ndarray, labels=None, n_threads: int = 1, chun
         # holds the GIL the threads share) is paid once per chunk, not once per cell
         chunk = max(32, min(128, -(-n // max(1, n_threads))))
     spans = [(i, min(n, i + chunk)) for i in range(0, n, chunk)]
+    if _lloyd_unwrapped is None and (labels is None or np.any(np.asarray(labels)[:, 0] < 0)):
+        # the public KMeans fallback sets and restores the BLAS thread count on every call,
+        # racing the BLAS calls of the other threads: those cells take one thread
+        n_threads = 1
     if n_threads <= 1 or len(spans) == 1:
         for lo, hi in spans:
             run(lo, hi)

@@ -235,3 +235,46 @@ def write_report(case: str, entry: dict, path: str = None):
     data[case] = entry
     with open(path, "w") as fh:
         json.dump(data, fh, indent=1, sort_keys=True)
+
+
+def decode_mismatches(prob, z, cn_dev, rep_dev, c: float = 8.0, nb_rel: float = 5e-6) -> dict:
+    """Account for every (bin, cell) whose decoded joint state (infer_discrete temperature 0,
+    pert_model.py:820-827) differs from the fp64 oracle's joint argmax at the same point.
+    Each such disagreement must be a near-tie: the oracle's score gap between its best state
+    B and the device's choice A, s(B) - s(A) >= 0, is set against the fp32 error bound of
+    the two scores, E(A) + E(B), with
+
+        E = c eps32 (|log pi~| + |log Bern| + |NB'| + delta |d NB'/d delta|) + nb_rel max(1, |NB'|)
+
+    (NB' = the reads term without its state-independent part kappa, the quantity the kernels
+    evaluate; nb_rel = the device special functions' accuracy, test_nb_lgdiff_device_accuracy;
+    the delta term covers delta's own fp32 rounding).  Returns the counts, the largest
+    gap / bound ratio (<= 1 when every mismatch is a near-tie) and the worst cases."""
+    from oracle import pert_oracle as po
+    eps = float(np.finfo(np.float32).eps)
+    with torch.no_grad():
+        t = po.enum_score_terms(prob, z)
+    P = prob.P
+    L, N = prob.reads.shape
+    nbp = t["lp_reads"] - t["kappa"]
+    E = (c * eps * (t["lp_cn"].abs() + t["lp_rep"].abs() + nbp.abs() + t["delta"] * t["dpsi"].abs())
+         + nb_rel * torch.clamp(nbp.abs(), min=1.0))
+    s = t["score"].reshape(2 * P, L, N).numpy()
+    E = E.reshape(2 * P, L, N).numpy()
+    best = np.argmax(s, axis=0)
+    cn_dev = np.asarray(cn_dev.cpu() if isinstance(cn_dev, torch.Tensor) else cn_dev).astype(np.int64)
+    rep_dev = np.asarray(rep_dev.cpu() if isinstance(rep_dev, torch.Tensor) else rep_dev).astype(np.int64)
+    dev = rep_dev * P + cn_dev
+    mism = np.argwhere(dev != best)
+    out = dict(n=int(L * N), mismatches=int(len(mism)), max_ratio=0.0, worst=[])
+    if len(mism):
+        li, ni = mism[:, 0], mism[:, 1]
+        b, a = best[li, ni], dev[li, ni]
+        gap = s[b, li, ni] - s[a, li, ni]
+        bound = E[b, li, ni] + E[a, li, ni]
+        ratio = gap / bound
+        order = np.argsort(-ratio)[:5]
+        out["max_ratio"] = float(ratio.max())
+        out["worst"] = [dict(bin=int(li[k]), cell=int(ni[k]), oracle_state=int(b[k]), device_state=int(a[k]),
+                             gap=float(gap[k]), bound=float(bound[k])) for k in order]
+    return out

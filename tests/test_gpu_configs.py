@@ -125,8 +125,13 @@ def test_c4_full_size_pass_per_cell_and_shared_parity():
                             **_bounds.floor_stats(ref_g["expose_pi"].numpy(), pf))
     rep["expose_pi"]["worst_delta_over_bound"] = _bounds.check("expose_pi", g["expose_pi"],
                                                                ref_g["expose_pi"].numpy(), pf)
+    # the decode of the sampled cells at the same point: every disagreement a near-tie
+    dec = _bounds.decode_mismatches(prob, z, cn1[:, torch.as_tensor(cells, device=cn1.device)],
+                                    rep1[:, torch.as_tensor(cells, device=rep1.device)])
     _bounds.write_report("c4_full_size_sampled_cells", {"kind": "step2", "shape": [L, N], "cells": cells.tolist(),
-                                                        "sites": rep})
+                                                        "sites": rep, "decode": dec})
+    assert dec["max_ratio"] <= 1.0, dec
+    assert dec["mismatches"] <= 1e-3 * dec["n"], dec
     for name, r in rep.items():
         assert r["rel_l2"] <= GRAD_RTOL, (name, r["rel_l2"])
     # shared sites: the full pass equals the sum of four disjoint shards (cuts on 64-cell

@@ -2,8 +2,9 @@
 
 Tolerances (BASELINE.json north_star, re-based on the fp64 restatement per SURVEY.md
 section 8c / Appendix C): loss within 1e-5 relative; every gradient ELEMENT within
-1e-4 relative plus the Appendix C floor (tests/_bounds.py); decode identical at the same
-parameters.  The reported-loss mode the product uses by default (dirichlet_mode
+1e-4 relative plus the Appendix C floor (tests/_bounds.py); decode at the same parameters
+equal to the oracle's joint argmax up to near-ties inside the fp32 score bound.  The
+reported-loss mode the product uses by default (dirichlet_mode
 'torch32', the reference's fp32 Dirichlet normaliser) is checked against the oracle's
 fp32-semantics constant.
 """
@@ -113,9 +114,16 @@ def test_adam_trajectory(kind, variant):
 @pytest.mark.parametrize("kind", ["step2", "step3"])
 def test_decode_matches_oracle(kind, variant):
     prob, kw, z = make_problem(kind, seed=11)
+    """Decode at fixed parameters: every disagreement with the fp64 oracle's joint argmax is a
+    near-tie within the fp32 error bound of the two scores (tests/_bounds.decode_mismatches),
+    and they are rare; the counts go to the parity report."""
     cn_ref, rep_ref = po.decode(prob, z)
     cn, rep = _shard(kind, kw, z, variant=variant).decode()
     agree = (cn.cpu().numpy() == cn_ref.numpy()) & (rep.cpu().numpy() == rep_ref.numpy())
+    acc = _bounds.decode_mismatches(prob, z, cn, rep)
+    _bounds.write_report("decode_{}_v{}".format(kind, variant), acc)
+    assert acc["mismatches"] == int((~agree).sum())
+    assert acc["max_ratio"] <= 1.0, acc
     assert agree.mean() >= 0.999, agree.mean()
 
 

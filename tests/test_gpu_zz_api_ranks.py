@@ -29,27 +29,33 @@ def _tables():
     return to_long_form(sim, n_libs=2)
 
 
-def _fit(**extra):
+def _fit(timings=None, **extra):
     from scdna_replication_tools.pert_model import pert_infer_scRT
     s, g = _tables()
     m = pert_infer_scRT(s, g, input_col='reads', clone_col='clone_id', cn_prior_method='g1_clones',
                         max_iter=120, min_iter=30, max_iter_step1=80, max_iter_step3=60, **extra)
-    return m.run_pert_model()
+    out = m.run_pert_model()
+    if timings is not None:
+        timings.update({k: v for k, v in m.timings.items() if isinstance(v, float)})
+    return out
 
 
 def _api_worker(rank, world, port, out_dir):
     import faulthandler
     import sys
-    faulthandler.dump_traceback_later(120, exit=True, file=sys.stderr)   # a hung rank shows where
+    # a hung rank shows where, well before the test's own deadline (90 s) and any runner limit
+    faulthandler.dump_traceback_later(60, exit=True, file=sys.stderr)
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{}".format(port), rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
-        cn_s, supp_s, cn_g, supp_g = _fit(device="cuda:0")
+        tm = {}
+        cn_s, supp_s, cn_g, supp_g = _fit(timings=tm, device="cuda:0")
         cols = ["model_cn_state", "model_rep_state", "model_tau", "model_u", "model_rho"]
         torch.save({"s": torch.as_tensor(cn_s[cols].to_numpy(np.float64)),
                     "g": torch.as_tensor(cn_g[cols].to_numpy(np.float64)),
                     "loss_s": torch.as_tensor(supp_s.loc[supp_s.param == "loss_s", "value"].to_numpy(np.float64)),
-                    "loss_g": torch.as_tensor(supp_s.loc[supp_s.param == "loss_g", "value"].to_numpy(np.float64))},
+                    "loss_g": torch.as_tensor(supp_s.loc[supp_s.param == "loss_g", "value"].to_numpy(np.float64)),
+                    "timings": tm},
                    os.path.join(out_dir, "api{}.pt".format(rank)))
     finally:
         dist.destroy_process_group()
@@ -62,15 +68,21 @@ def test_run_pert_model_two_ranks_match_single_rank(tmp_path):
     calls and per-cell sites)."""
     import time
     ctx = mp.spawn(_api_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=False)
-    deadline = time.time() + 200          # bounded: a hung rank fails the test instead of the suite
+    deadline = time.time() + 90           # bounded: a hung rank fails the test instead of the suite
     while not ctx.join(timeout=5):
         if time.time() > deadline:
             for p in ctx.processes:
                 if p.is_alive():
                     p.kill()
-            pytest.fail("the two ranks did not finish within 200 s")
+            pytest.fail("the two ranks did not finish within 90 s")
     r = [torch.load(str(tmp_path / "api{}.pt".format(i)), weights_only=True) for i in range(2)]
-    cn_s, supp_s, cn_g, supp_g = _fit()
+    tm1 = {}
+    cn_s, supp_s, cn_g, supp_g = _fit(timings=tm1)
+    from tests._bounds import write_report
+    keys = ("helper_guess_times_s", "helper_guess_times_g", "helper_priors", "total")
+    write_report("api_two_ranks_timings", {"one_rank": {k: tm1.get(k) for k in keys},
+                                           "rank0": {k: r[0]["timings"].get(k) for k in keys},
+                                           "rank1": {k: r[1]["timings"].get(k) for k in keys}})
     cols = ["model_cn_state", "model_rep_state", "model_tau", "model_u", "model_rho"]
     for i in range(2):
         for name, ref in (("s", cn_s), ("g", cn_g)):

@@ -286,6 +286,11 @@ def main():
                          "g1_composite (the reference's default; the product's composite code book, many rows)")
     ap.add_argument("--event-stride", type=int, default=5,
                     help="HIP events around the pass of every k-th timed step (1: every step)")
+    ap.add_argument("--comm", default="auto", choices=["auto", "rccl", "torch"],
+                    help="cross-rank sum of the shared block: 'rccl' = the library's own RCCL communicator "
+                         "(pert_comm, queued inside the C loop; the default on N > 1 over nccl, and at N = 1 "
+                         "it times the sharded step with a one-rank all-reduce), 'torch' = torch.distributed "
+                         "per step from Python")
     ap.add_argument("--cpu-cells", type=int, default=640)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -317,7 +322,7 @@ def main():
             dist.init_process_group(backend)
         pg = dist
 
-    from scdna_replication_tools_amd.engine import EtaCodebook, PertShard
+    from scdna_replication_tools_amd.engine import EtaCodebook, PertShard, RcclComm
     from scdna_replication_tools_amd.init import init_params
     from scdna_replication_tools_amd.sharding import cell_bounds, make_allreduce
 
@@ -352,10 +357,16 @@ def main():
         t_init = np.clip(data["tau"][n0:n1].cpu().numpy(), 0.05, 0.95)
         prior_desc = "g1_clones (weight 1e6)"
     ploidy = eta.argmax_states().mean(0)
-    allreduce = make_allreduce()
+    comm = None
+    if args.comm == "rccl" or (args.comm == "auto" and world > 1 and backend == "nccl"):
+        comm = RcclComm() if world > 1 else RcclComm.world1()
+    allreduce = comm.allreduce if comm is not None else make_allreduce()
+    comm_desc = ("rccl: the library's own communicator, all-reduce queued inside the C loop (pert_svi_run_sharded)"
+                 if comm is not None else "torch.distributed all_reduce per step from Python" if allreduce is not None
+                 else "none (one rank)")
     libs = np.zeros(n1 - n0, int)
     common = dict(device=device, is_root=(rank == 0), allreduce=allreduce, bins_per_tile=args.bins_per_tile,
-                  variant=args.variant, fused=args.fused and not args.no_fused)
+                  variant=args.variant, fused=args.fused and not args.no_fused, comm=comm)
     if args.fit == "step1":
         # step 1 (pert_model.py:718-774): the same cells as G1/2 cells, doubled with rep 0 / 1 --
         # as the product runs it, in pair mode (the columns stored once, both copies per lane)
@@ -400,18 +411,35 @@ def main():
     if pg is not None:
         pg.barrier()
     dt = time.perf_counter() - t0
+    dt_plain = None
     if shard.pass_events is None:
         shard.pass_events = []
         shard.run_svi(10, min_iter=10 ** 9, rel_tol=0.0)
+    else:
+        # the same K steps again on the production host path (no events: one C call for the
+        # whole loop), as a cross-check of the timed region's host path
+        events, shard.pass_events = shard.pass_events, None
+        shard.reserve_svi(args.steps)
+        if pg is not None:
+            pg.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        shard.run_svi(args.steps, min_iter=10 ** 9, rel_tol=0.0)
+        torch.cuda.synchronize()
+        if pg is not None:
+            pg.barrier()
+        dt_plain = time.perf_counter() - t1
+        shard.pass_events = events
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in shard.pass_events]))
     shard.pass_events = None
     # after the timed region: the same shard's HBM streams with no arithmetic (the pattern's
     # ceiling on this device, this lease) -- pert_stream_ceiling leaves the state unchanged
     ceil_ms = shard.stream_ceiling_ms() if args.fit != "step1" else None
-    t = torch.tensor([dt, kern_ms], dtype=torch.float64, device=device)
+    t = torch.tensor([dt, kern_ms, dt_plain if dt_plain is not None else -1.0], dtype=torch.float64, device=device)
     if pg is not None:
         pg.all_reduce(t, op=pg.ReduceOp.MAX)
     dt, kern_ms_max = float(t[0]), float(t[1])
+    dt_plain = float(t[2]) if dt_plain is not None else None
 
     if rank == 0:
         cellbins_total = L * n_total * (2 if args.fit == "step1" else 1)
@@ -443,7 +471,15 @@ def main():
             "scaling": args.scaling, "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": desc, "config": args.config, "cells": n_total, "bins": L, "P": P,
                        "K": K, "cn_prior": prior_desc, "parallelism": "cell-sharded x{}".format(world),
-                       "bins_per_tile": shard.bins_per_tile, "fit": args.fit},
+                       "bins_per_tile": shard.bins_per_tile, "fit": args.fit, "allreduce": comm_desc,
+                       "timed_loop": ("pert_svi_steps{} chunks of 8 iterations per GIL-free C call, HIP events "
+                                      "around every {}th pass".format("_sharded" if comm is not None else "",
+                                                                      args.event_stride)
+                                      if args.event_stride > 0 and (comm is not None or allreduce is None)
+                                      else "pert_svi_run{}: the whole loop in one GIL-free C call".format(
+                                          "_sharded" if comm is not None else "")
+                                      if comm is not None or allreduce is None
+                                      else "per-iteration launches from Python")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
                          "kernel": ("obs_kernel" if step1 else
@@ -460,6 +496,8 @@ def main():
                          "valu_issue_frac": (valu or {}).get("issue_frac")},
             "loss_first": losses[0], "loss_last": losses[-1],
         }
+        if dt_plain is not None:
+            rec["ms_per_step_no_events"] = dt_plain / args.steps * 1e3
         if ceil_ms is not None:
             rec["roofline"]["pattern_ceiling"] = {
                 "ms": ceil_ms, "GB/s": bpc * local_cb / (ceil_ms * 1e-3) / 1e9,
@@ -496,6 +534,8 @@ def main():
         else:
             rec["cpu_baseline"] = None
         print(json.dumps(rec), flush=True)
+    if comm is not None:
+        comm.close()
     if pg is not None:
         pg.destroy_process_group()
 

@@ -62,7 +62,9 @@ extern "C" {
 #define PERT_E_ARG 1
 #define PERT_E_UNSUPPORTED_P 2
 #define PERT_E_UNSUPPORTED_K 3
-#define PERT_E_HIP_BASE 1000
+#define PERT_E_COMM_UNAVAILABLE 5   /* RCCL not loaded (pert_comm_load) or lacks a symbol */
+#define PERT_E_HIP_BASE 1000        /* + hipError_t */
+#define PERT_E_COMM_BASE 2000       /* + ncclResult_t */
 
 #define PERT_MAX_K1 8      /* K + 1 <= 8 */
 #define PERT_MIN_P 2
@@ -241,6 +243,41 @@ int pert_svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hpara
                  const float* step_size, const float* inv_bc2_sqrt, int32_t n_iter, int32_t chunk,
                  int32_t depth, int32_t one_launch, double* host_rec, int32_t* n_launched,
                  hipStream_t stream);
+
+/* ---- Sharded fits: cells split over ranks, one process per GPU.
+ * The shared block's gradient [0, n_shared) and the loss (slot n_shared) are summed across
+ * the ranks once per SVI step, between the reductions and Adam.  A pert_comm is an RCCL
+ * communicator over the fit's ranks (xGMI): the library queues that all-reduce itself on
+ * the fit's stream, so a whole sharded fit is one C call like a single-rank one. */
+typedef struct pert_comm pert_comm;
+
+/* dlopen RCCL from rccl_path (the copy the process already uses -- torch's) and resolve
+ * ncclGetUniqueId / ncclCommInitRank / ncclAllReduce / ncclCommDestroy.  Once per process. */
+int pert_comm_load(const char* rccl_path);
+/* ncclGetUniqueId into id (n = 128 bytes), on one rank; the caller broadcasts it. */
+int pert_comm_unique_id(uint8_t* id, int32_t n);
+/* ncclCommInitRank on the current device (collective: returns once every rank has called). */
+int pert_comm_init(const uint8_t* id, int32_t n, int32_t world, int32_t rank, pert_comm** out);
+int pert_comm_destroy(pert_comm* comm);
+/* recv = sum over ranks of send (fp64, n elements; send == recv allowed), queued on stream. */
+int pert_comm_allreduce_sum_f64(pert_comm* comm, const double* send, double* recv, int64_t n,
+                                hipStream_t stream);
+
+/* pert_svi_steps / pert_svi_run of one rank of a sharded fit: each step's reductions write
+ * this shard's shared-block sums to grad_local ([n_shared + 1] doubles), pert_comm_allreduce_sum_f64
+ * sums them over the ranks into st->grad_shared, then Adam runs on the summed block
+ * (pert_enum_step(update_shared = 0) + all-reduce + pert_adam_shared when one_launch; else
+ * pass, pert_finalize, all-reduce, pert_adam).  Every rank stops after the same iteration
+ * (the loss the rule tests is the all-reduced one) and queues the same number of
+ * all-reduces.  Replaces the svi_s.step() loop of pert_model.py:800-816 on a cell shard. */
+int pert_svi_steps_sharded(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
+                           const float* step_size, const float* inv_bc2_sqrt, int32_t iter0, int32_t n,
+                           int32_t one_launch, pert_comm* comm, double* grad_local,
+                           hipEvent_t* pass_events, hipStream_t stream);
+int pert_svi_run_sharded(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
+                         const float* step_size, const float* inv_bc2_sqrt, int32_t n_iter, int32_t chunk,
+                         int32_t depth, int32_t one_launch, pert_comm* comm, double* grad_local,
+                         double* host_rec, int32_t* n_launched, hipStream_t stream);
 
 /* Diagnostic (bench.py): the HBM streams of pert_enum_pass(PERT_MODE_STEP) -- x, eta code,
  * z/m/v read and written back unchanged, same grid and tile length -- with no arithmetic.

@@ -28,7 +28,8 @@ EXPORTED_SYMBOLS = (
     "pert_make_layout", "pert_workspace_sizes", "pert_auto_bins_per_tile", "pert_enum_pass", "pert_obs_pass",
     "pert_finalize", "pert_adam", "pert_enum_step", "pert_adam_shared", "pert_stream_ceiling", "pert_selftest_nb_lgdiff_host",
     "pert_selftest_nb_lgdiff_device", "pert_selftest_enum_cellbin_host", "pert_tau_binarize", "pert_svi_steps",
-    "pert_svi_run", "pert_version",
+    "pert_svi_run", "pert_comm_load", "pert_comm_unique_id", "pert_comm_init", "pert_comm_destroy",
+    "pert_comm_allreduce_sum_f64", "pert_svi_steps_sharded", "pert_svi_run_sharded", "pert_version",
 )
 
 
@@ -166,6 +167,16 @@ def load(path: str, gil: bool = True):
                                       i32, i32, i32, c_void_p, c_void_p]
     handle.pert_svi_run.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams), fp, fp,
                                     i32, i32, i32, i32, c_void_p, POINTER(i32), c_void_p]
+    handle.pert_comm_load.argtypes = [c_char_p]
+    handle.pert_comm_unique_id.argtypes = [c_void_p, i32]
+    handle.pert_comm_init.argtypes = [c_void_p, i32, i32, i32, POINTER(c_void_p)]
+    handle.pert_comm_destroy.argtypes = [c_void_p]
+    handle.pert_comm_allreduce_sum_f64.argtypes = [c_void_p, c_void_p, c_void_p, i64, c_void_p]
+    handle.pert_svi_steps_sharded.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams), fp,
+                                              fp, i32, i32, i32, c_void_p, c_void_p, c_void_p, c_void_p]
+    handle.pert_svi_run_sharded.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams), fp,
+                                            fp, i32, i32, i32, i32, c_void_p, c_void_p, c_void_p, POINTER(i32),
+                                            c_void_p]
     handle.pert_selftest_nb_lgdiff_host.argtypes = [i64, fp, fp, fp, fp]
     handle.pert_selftest_nb_lgdiff_device.argtypes = [i64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     handle.pert_selftest_enum_cellbin_host.argtypes = [i32, i64, fp, fp, fp, fp, c_float, fp, fp, fp, fp,
@@ -181,8 +192,12 @@ def load(path: str, gil: bool = True):
 
 def check(code: int, what: str):
     if code != 0:
+        if code >= 2000:
+            raise RuntimeError("{} failed: RCCL error {}".format(what, code - 2000))
         if code >= 1000:
             raise RuntimeError("{} failed: HIP error {}".format(what, code - 1000))
+        if code == 5:
+            raise NativeLibraryError("{} failed: RCCL is not loaded (pert_comm_load)".format(what))
         raise ValueError("{} failed: status {}".format(what, code))
 
 

@@ -20,7 +20,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SOURCES = [os.path.join(HERE, "csrc", "pert_kernels.hip"), os.path.join(HERE, "csrc", "tau_kernels.hip")]
+SOURCES = [os.path.join(HERE, "csrc", "pert_kernels.hip"), os.path.join(HERE, "csrc", "tau_kernels.hip"),
+           os.path.join(HERE, "csrc", "pert_comm.hip")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", "pert_math.h"), os.path.join(ROOT, "include", "pert_hip.h")]
 OUT = os.path.join(HERE, "libpert_hip.so")
 OBJ_DIR = os.path.join(HERE, "build_obj")

@@ -2390,41 +2390,59 @@ int pert_adam(const pert_problem* prob, pert_state* st, const pert_adam_hparams*
   return hip_status(hipGetLastError());
 }
 
-int pert_svi_steps(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp, const float* step_size,
-                   const float* inv_bc2_sqrt, int32_t iter0, int32_t n, int32_t one_launch, hipEvent_t* pass_events,
-                   hipStream_t stream) {
+}  // extern "C"
+
+namespace {
+
+// n SVI steps from loop iteration iter0; comm != NULL: one rank of a sharded fit (the shard's
+// shared-block sums into grad_local, summed over the ranks into st->grad_shared before Adam)
+int svi_steps(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp, const float* step_size,
+              const float* inv_bc2_sqrt, int32_t iter0, int32_t n, int32_t one_launch, pert_comm* comm,
+              double* grad_local, hipEvent_t* pass_events, hipStream_t stream) {
   if (!problem_ok(prob) || !st || !hp || !step_size || !inv_bc2_sqrt || n < 0 || iter0 < 0) return PERT_E_ARG;
+  if (comm && (!grad_local || !st->grad_shared || grad_local == st->grad_shared)) return PERT_E_ARG;
   const bool enumerated = prob->kind == PERT_KIND_STEP2 || prob->kind == PERT_KIND_STEP3;
   if (one_launch && (!enumerated || st->variant != 3)) return PERT_E_ARG;
   pert_state s = *st;
+  pert_state s_loc = *st;                      // the reductions' view: grad_shared -> grad_local
+  if (comm) s_loc.grad_shared = grad_local;
   pert_adam_hparams h = *hp;
+  const int64_t n_sum = (int64_t)st->lay.n_shared + 1;
   int rc = PERT_OK;
   auto mark = [&](int32_t i, int which) {
     if (pass_events && pass_events[2 * i + which] && rc == PERT_OK)
       rc = hip_status(hipEventRecord(pass_events[2 * i + which], stream));
   };
+  auto all_reduce = [&]() {
+    if (rc == PERT_OK) rc = pert_comm_allreduce_sum_f64(comm, grad_local, st->grad_shared, n_sum, stream);
+  };
   for (int32_t i = 0; i < n && rc == PERT_OK; ++i) {
-    s.step = iter0 + i;                        // the loop record's iteration index
+    s.step = s_loc.step = iter0 + i;           // the loop record's iteration index
     h.step_size = step_size[i];
     h.inv_bc2_sqrt = inv_bc2_sqrt[i];
     mark(i, 0);
     if (one_launch) {
-      if (rc == PERT_OK) rc = pert_enum_step(prob, &s, &h, 1, stream);
+      if (rc == PERT_OK) rc = pert_enum_step(prob, comm ? &s_loc : &s, &h, comm ? 0 : 1, stream);
       mark(i, 1);
+      if (comm) {
+        all_reduce();
+        if (rc == PERT_OK) rc = pert_adam_shared(prob, &s, &h, stream);
+      }
       continue;
     }
     if (rc == PERT_OK)
       rc = enumerated ? pert_enum_pass(prob, &s, &h, PERT_MODE_STEP, stream) : pert_obs_pass(prob, &s, stream);
     mark(i, 1);
-    if (rc == PERT_OK) rc = pert_finalize(prob, &s, stream);
+    if (rc == PERT_OK) rc = pert_finalize(prob, comm ? &s_loc : &s, stream);
+    if (comm) all_reduce();
     if (rc == PERT_OK) rc = pert_adam(prob, &s, &h, stream);
   }
   return rc;
 }
 
-int pert_svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp, const float* step_size,
-                 const float* inv_bc2_sqrt, int32_t n_iter, int32_t chunk, int32_t depth, int32_t one_launch,
-                 double* host_rec, int32_t* n_launched, hipStream_t stream) {
+int svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp, const float* step_size,
+            const float* inv_bc2_sqrt, int32_t n_iter, int32_t chunk, int32_t depth, int32_t one_launch,
+            pert_comm* comm, double* grad_local, double* host_rec, int32_t* n_launched, hipStream_t stream) {
   if (!st || !st->loop_ctl || !st->loop_rec || !host_rec || !n_launched || n_iter < 0 || chunk < 1 || depth < 1)
     return PERT_E_ARG;
   *n_launched = 0;
@@ -2439,7 +2457,9 @@ int pert_svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hpara
   int waited = 0;                              // chunks whose records have been looked at
   bool stop_seen = false;
   int c = 0;
-  // a chunk's records are at host_rec[2 j] (loss) and host_rec[2 j + 1] (>= 0: stopped at j)
+  // a chunk's records are at host_rec[2 j] (loss) and host_rec[2 j + 1] (>= 0: stopped at j).
+  // Which chunks are looked at, and when, depends only on the chunk index: the ranks of a
+  // sharded fit (identical, all-reduced loss records) stop queueing after the same chunk.
   auto look = [&](int k) {
     rc = rc == PERT_OK ? hip_status(hipEventSynchronize(ev[k % ring])) : rc;
     const int j1 = (k + 1) * chunk < n_iter ? (k + 1) * chunk : n_iter;
@@ -2450,7 +2470,8 @@ int pert_svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hpara
     if (c - waited >= ring - 1) look(waited++);          // the ring's oldest chunk is done
     if (stop_seen || rc != PERT_OK) break;
     const int j0 = c * chunk, n = (j0 + chunk < n_iter ? j0 + chunk : n_iter) - j0;
-    rc = pert_svi_steps(prob, st, hp, step_size + j0, inv_bc2_sqrt + j0, j0, n, one_launch, nullptr, stream);
+    rc = svi_steps(prob, st, hp, step_size + j0, inv_bc2_sqrt + j0, j0, n, one_launch, comm, grad_local, nullptr,
+                   stream);
     if (rc == PERT_OK)
       rc = hip_status(hipMemcpyAsync(host_rec + 2 * j0, st->loop_rec + 2 * j0, sizeof(double) * 2 * n,
                                      hipMemcpyDeviceToHost, stream));
@@ -2461,6 +2482,40 @@ int pert_svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hpara
   if (rc == PERT_OK) rc = hip_status(e);
   for (int k = 0; k < made; ++k) (void)hipEventDestroy(ev[k]);
   return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pert_svi_steps(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp, const float* step_size,
+                   const float* inv_bc2_sqrt, int32_t iter0, int32_t n, int32_t one_launch, hipEvent_t* pass_events,
+                   hipStream_t stream) {
+  return svi_steps(prob, st, hp, step_size, inv_bc2_sqrt, iter0, n, one_launch, nullptr, nullptr, pass_events, stream);
+}
+
+int pert_svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp, const float* step_size,
+                 const float* inv_bc2_sqrt, int32_t n_iter, int32_t chunk, int32_t depth, int32_t one_launch,
+                 double* host_rec, int32_t* n_launched, hipStream_t stream) {
+  return svi_run(prob, st, hp, step_size, inv_bc2_sqrt, n_iter, chunk, depth, one_launch, nullptr, nullptr, host_rec,
+                 n_launched, stream);
+}
+
+int pert_svi_steps_sharded(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
+                           const float* step_size, const float* inv_bc2_sqrt, int32_t iter0, int32_t n,
+                           int32_t one_launch, pert_comm* comm, double* grad_local, hipEvent_t* pass_events,
+                           hipStream_t stream) {
+  if (!comm) return PERT_E_ARG;
+  return svi_steps(prob, st, hp, step_size, inv_bc2_sqrt, iter0, n, one_launch, comm, grad_local, pass_events, stream);
+}
+
+int pert_svi_run_sharded(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
+                         const float* step_size, const float* inv_bc2_sqrt, int32_t n_iter, int32_t chunk,
+                         int32_t depth, int32_t one_launch, pert_comm* comm, double* grad_local, double* host_rec,
+                         int32_t* n_launched, hipStream_t stream) {
+  if (!comm) return PERT_E_ARG;
+  return svi_run(prob, st, hp, step_size, inv_bc2_sqrt, n_iter, chunk, depth, one_launch, comm, grad_local, host_rec,
+                 n_launched, stream);
 }
 
 int pert_stream_ceiling(const pert_problem* prob, pert_state* st, hipStream_t stream) {

@@ -270,6 +270,70 @@ class CanonicalPiBlock:
         return c["lp"][t - 1] if t > 0 else float("nan")
 
 
+# --------------------------------------------------------------------------- ranks
+def rccl_path() -> str:
+    """The RCCL library this process already uses (torch's, which libtorch_hip links): the
+    communicator of a sharded fit is made with the same copy."""
+    try:
+        with open("/proc/self/maps") as fh:
+            for line in fh:
+                path = line.split()[-1] if line.strip() else ""
+                if "/librccl.so" in path:
+                    return path
+    except OSError:
+        pass
+    import os
+    return os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+
+
+class RcclComm:
+    """An RCCL communicator over the ranks of a sharded fit (``pert_comm``, include/pert_hip.h):
+    the library queues the per-step all-reduce of the shared block itself, on the fit's stream,
+    so a sharded fit's SVI loop is one GIL-free C call (``pert_svi_run_sharded``) as a
+    single-rank one is.  Made collectively by every rank of ``group`` (rank 0's unique id
+    broadcast over the group), on the current device; ``world1()`` makes a one-rank
+    communicator without a process group (tests, bench)."""
+
+    def __init__(self, group=None, *, world1: bool = False):
+        self.lib = nat.lib_nogil()              # init blocks until every rank has called: GIL released
+        nat.check(self.lib.pert_comm_load(rccl_path().encode()), "pert_comm_load")
+        if world1:
+            self.world, self.rank, dist = 1, 0, None
+        else:
+            import torch.distributed as dist
+            self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        uid = (ctypes.c_uint8 * 128)()
+        if self.rank == 0:
+            nat.check(self.lib.pert_comm_unique_id(uid, 128), "pert_comm_unique_id")
+        if dist is not None and self.world > 1:
+            dev = (torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl"
+                   else torch.device("cpu"))
+            t = torch.tensor(list(bytes(uid)), dtype=torch.uint8, device=dev)
+            dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+            uid = (ctypes.c_uint8 * 128)(*t.cpu().tolist())
+        h = ctypes.c_void_p()
+        nat.check(self.lib.pert_comm_init(uid, 128, self.world, self.rank, ctypes.byref(h)), "pert_comm_init")
+        self.handle = h
+
+    @classmethod
+    def world1(cls) -> "RcclComm":
+        return cls(world1=True)
+
+    def allreduce(self, t: torch.Tensor) -> None:
+        """In-place sum over the ranks of an fp64 device tensor, on the current stream."""
+        if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("RcclComm.allreduce takes a contiguous fp64 device tensor")
+        nat.check(self.lib.pert_comm_allreduce_sum_f64(self.handle, t.data_ptr(), t.data_ptr(), t.numel(),
+                                                        torch.cuda.current_stream(t.device).cuda_stream),
+                  "pert_comm_allreduce_sum_f64")
+
+    def close(self) -> None:
+        if self.handle is not None and self.handle.value:
+            torch.cuda.synchronize()
+            nat.check(self.lib.pert_comm_destroy(self.handle), "pert_comm_destroy")
+        self.handle = None
+
+
 # --------------------------------------------------------------------------- shard
 def _ptr(t: Optional[torch.Tensor]) -> int:
     return 0 if t is None else int(t.data_ptr())
@@ -285,7 +349,7 @@ class PertShard:
                  is_root: bool = True, n_cells_total: Optional[int] = None,
                  allreduce: Optional[Callable[[torch.Tensor], None]] = None,
                  dirichlet_mode: str = "torch32", bins_per_tile: int = 0, variant: int = 3, fused: bool = False,
-                 paired: bool = False, lib=None):
+                 paired: bool = False, lib=None, comm: Optional[RcclComm] = None):
         self.lib = nat.lib() if lib is None else lib        # another build of the ABI (A/B tools)
         # the chunked SVI loop's handle: the product library through CDLL (the call releases the
         # GIL while it queues its launches); an A/B build keeps its own handle
@@ -315,7 +379,10 @@ class PertShard:
             raise ValueError("K={} unsupported (K+1 <= 8)".format(K))
         self.n_cells_total = N if n_cells_total is None else int(n_cells_total)
         self.lr, self.betas, self.eps = float(lr), tuple(betas), float(eps)
-        self.allreduce = allreduce
+        # a pert_comm communicator: the SVI loop (run_svi) queues the all-reduce in the library
+        # (pert_svi_run_sharded); single steps and the set-up constants use it from here
+        self.comm = comm
+        self.allreduce = comm.allreduce if (comm is not None and allreduce is None) else allreduce
         self.t = 0
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
@@ -373,7 +440,7 @@ class PertShard:
         self.adam_v = torch.zeros(lay.n_params, **f32)
         self.grad_shared = torch.zeros(lay.n_shared + 1, dtype=torch.float64, device=dev)
         # this shard's own shared-block sums (all-reduced into grad_shared when sharded)
-        self.grad_local = torch.zeros_like(self.grad_shared) if allreduce is not None else self.grad_shared
+        self.grad_local = torch.zeros_like(self.grad_shared) if self.allreduce is not None else self.grad_shared
         self.grad_cell = torch.zeros(lay.n_params - lay.n_shared, **f32)
         self._load_init(init)
 
@@ -720,12 +787,16 @@ class PertShard:
         st = self._state
         st.loop_ctl, st.loop_rec, st.loss_offset = _ptr(ctl), _ptr(rec), _ptr(offs)
         st.loss_const, st.rel_tol, st.min_iter = float(self.const_total), float(rel_tol), int(min_iter)
-        # one rank: the whole loop is ONE C call (pert_svi_run) that releases the GIL for the fit's
-        # duration -- a helper thread's Python work never delays the queueing of steps; with
-        # per-pass timing events (pass_events, bench.py) a chunk of iterations per C call
-        # (pert_svi_steps, the events recorded around each pass); sharded, per iteration from
-        # Python (the all-reduce sits between the reductions and Adam)
-        chunked = self.allreduce is None and self._lib_chunk is not None
+        # one rank, or ranks joined by a pert_comm: the whole loop is ONE C call (pert_svi_run /
+        # pert_svi_run_sharded, the all-reduce queued by the library) that releases the GIL for
+        # the fit's duration -- a helper thread's Python work never delays the queueing of steps;
+        # with per-pass timing events (pass_events, bench.py) a chunk of iterations per C call
+        # (pert_svi_steps[_sharded], the events recorded around each pass); sharded over another
+        # process group (gloo), per iteration from Python (torch.distributed's all-reduce sits
+        # between the reductions and Adam)
+        native_comm = self.comm is not None and self.allreduce == self.comm.allreduce
+        chunked = (self.allreduce is None or native_comm) and self._lib_chunk is not None
+        shard_args = (self.comm.handle, _ptr(self.grad_local)) if native_comm else ()
         b1, b2 = self.betas
         launched = 0
         pending = []
@@ -735,12 +806,14 @@ class PertShard:
                 ss = np.array([self.lr / (1.0 - b1 ** t) for t in ts], dtype=F32)         # as _set_hparams
                 ib = np.array([1.0 / math.sqrt(1.0 - b2 ** t) for t in ts], dtype=F32)
                 nl = ctypes.c_int32(0)
+                fn = self._lib_chunk.pert_svi_run_sharded if native_comm else self._lib_chunk.pert_svi_run
                 with self._dev():
-                    nat.check(self._lib_chunk.pert_svi_run(
+                    nat.check(fn(
                         ctypes.byref(self._prob), ctypes.byref(st), ctypes.byref(self._hp),
                         ss.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
                         ib.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n, chunk, depth,
-                        1 if self.fused else 0, host.data_ptr(), ctypes.byref(nl), self._stream()), "pert_svi_run")
+                        1 if self.fused else 0, *shard_args, host.data_ptr(), ctypes.byref(nl), self._stream()),
+                        "pert_svi_run")
                 launched = int(nl.value)
                 n = 0                              # nothing left for the chunk loop below
             for j0 in range(0, n, chunk):
@@ -761,12 +834,13 @@ class PertShard:
                                 ptrs[2 * (i - j0)], ptrs[2 * (i - j0) + 1] = e0.cuda_event, e1.cuda_event
                                 self.pass_events.append((e0, e1))
                         evp = (ctypes.c_void_p * len(ptrs))(*ptrs)
+                    fn = self._lib_chunk.pert_svi_steps_sharded if native_comm else self._lib_chunk.pert_svi_steps
                     with self._dev():
-                        nat.check(self._lib_chunk.pert_svi_steps(
+                        nat.check(fn(
                             ctypes.byref(self._prob), ctypes.byref(st), ctypes.byref(self._hp),
                             ss.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
                             ib.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), j0, j1 - j0, 1 if self.fused else 0,
-                            evp, self._stream()), "pert_svi_steps")
+                            *shard_args, evp, self._stream()), "pert_svi_steps")
                 else:
                     for i in range(j0, j1):
                         st.step = i

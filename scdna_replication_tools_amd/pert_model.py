@@ -118,8 +118,21 @@ class _Dist:
         self.group = group
         self.world = self.dist.get_world_size(group) if self.dist else 1
         self.rank = self.dist.get_rank(group) if self.dist else 0
-        self.allreduce = make_allreduce(group) if self.world > 1 else None
         self.backend = self.dist.get_backend(group) if self.dist else None
+        # ranks on RCCL (one process per GPU): a pert_comm communicator of the library's own, so
+        # each fit's SVI loop -- all-reduce included -- is one GIL-free C call; other backends
+        # (gloo: several ranks sharing a GPU in tests) all-reduce through torch.distributed per step
+        self.comm = None
+        if self.world > 1 and self.backend == "nccl" and os.environ.get("PERT_NATIVE_COMM", "1") != "0":
+            from .engine import RcclComm
+            self.comm = RcclComm(group)
+        self.allreduce = (self.comm.allreduce if self.comm is not None else
+                          make_allreduce(group) if self.world > 1 else None)
+
+    def close(self):
+        if self.comm is not None:
+            self.comm.close()
+            self.comm = None
 
     def bounds(self, n: int):
         return cell_bounds(n, self.world)[self.rank]
@@ -409,7 +422,7 @@ class pert_infer_scRT():
         return PertShard(kind, np.ascontiguousarray(reads[:, sl]), self._inp.gc, np.asarray(libs)[sl], self.L,
                          self.P, self.K, self._cells(init, sl, N), eta=eta, device=self.device, lr=self.learning_rate,
                          dirichlet_mode=self.dirichlet_mode, is_root=dd.rank == 0, n_cells_total=N,
-                         allreduce=dd.allreduce, **kw)
+                         allreduce=dd.allreduce, comm=dd.comm, **kw)
 
     def _shard_pairs(self, dd: _Dist, reads_g, states_g, libs2, init):
         """Step 1's PertShard in pair mode over this rank's contiguous range of G1/2 cells:
@@ -422,7 +435,7 @@ class pert_infer_scRT():
         return PertShard(KIND_STEP1, np.ascontiguousarray(reads_g[:, a:b]), self._inp.gc, np.asarray(libs2)[idx],
                          self.L, self.P, self.K, cells, cn_obs=np.ascontiguousarray(states_g[:, a:b]), paired=True,
                          device=self.device, lr=self.learning_rate, dirichlet_mode=self.dirichlet_mode,
-                         is_root=dd.rank == 0, n_cells_total=2 * NG, allreduce=dd.allreduce)
+                         is_root=dd.rank == 0, n_cells_total=2 * NG, allreduce=dd.allreduce, comm=dd.comm)
 
     def _decode(self, shard: PertShard, dd: _Dist):
         cn, rep = shard.decode()
@@ -590,6 +603,7 @@ class pert_infer_scRT():
             # also when a fit or a helper task raised: no helper work outlives the call
             helper.shutdown(wait=True, cancel_futures=True)
             threads.close()
+            dd.close()
         self.timings["total"] = time.perf_counter() - t_all
         return cn_s_out, supp_s_out_df, cn_g1_out, supp_g1_out_df
 

@@ -1,0 +1,74 @@
+"""GPU: the library's own RCCL communicator (pert_comm, include/pert_hip.h) driving a sharded
+fit's whole SVI loop in C (pert_svi_run_sharded / pert_svi_steps_sharded: reductions into the
+shard's grad_local, the all-reduce queued on the fit's stream, Adam) against the same sharded
+step driven per iteration from Python (PertShard with a Python all-reduce).  One GPU, so the
+communicator is a one-rank RCCL world (a sum over one rank is the identity): both loops run
+the same kernels on the same state, and the loss traces, the stopping iteration and the final
+parameters must be identical bit for bit.  The multi-GPU bench runs the same path at N = 2..8.
+"""
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from tests._problems import KIND_OF, init_constrained, make_problem
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def comm():
+    from scdna_replication_tools_amd.engine import RcclComm
+    c = RcclComm.world1()
+    yield c
+    c.close()
+
+
+def _shard(kind, kw, z, **extra):
+    from scdna_replication_tools_amd.engine import PertShard
+    sh = PertShard(KIND_OF[kind], init=init_constrained(kind, z), device="cuda", **kw, **extra)
+    sh.set_unconstrained({k: v.numpy() for k, v in z.items()})
+    return sh
+
+
+def _state(sh):
+    out = {k: np.asarray(v) for k, v in sh.constrained().items()}
+    if sh.z_pi is not None:
+        out["z_pi"] = sh.z_pi.cpu().numpy()
+    return out
+
+
+def test_comm_allreduce_world1_is_identity(comm):
+    t = torch.arange(5452, dtype=torch.float64, device="cuda") * 0.37
+    want = t.clone()
+    comm.allreduce(t)
+    torch.cuda.synchronize()
+    assert torch.equal(t, want)
+    n = 200
+    t0 = time.perf_counter()
+    for _ in range(n):
+        comm.allreduce(t)
+    torch.cuda.synchronize()
+    print("pert_comm all-reduce of 5,452 fp64 (world 1): {:.1f} us per call".format(
+        (time.perf_counter() - t0) / n * 1e6))
+
+
+@pytest.mark.parametrize("kind,fused", [("step2", False), ("step2", True), ("step3", True), ("step1p", False)])
+@pytest.mark.parametrize("events", [False, True])
+def test_native_sharded_loop_matches_python_sharded_loop(comm, kind, fused, events):
+    prob, kw, z = make_problem(kind, seed=4)
+    a = _shard(kind, kw, z, fused=fused, comm=comm)
+    b = _shard(kind, kw, z, fused=fused, allreduce=lambda t: None)     # per-iteration Python loop
+    assert a.comm is comm and b.comm is None
+    if events:
+        a.pass_events, a.pass_event_stride = [], 3
+    la, ra = a.run_svi(60, 12, 5e-2)
+    lb, rb = b.run_svi(60, 12, 5e-2)
+    assert (ra, len(la)) == (rb, len(lb))
+    assert np.array_equal(np.asarray(la), np.asarray(lb))
+    sa, sb = _state(a), _state(b)
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
+    if events:
+        assert len(a.pass_events) >= len(la) // 3

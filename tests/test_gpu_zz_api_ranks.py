@@ -37,6 +37,8 @@ def _fit(timings=None, **extra):
     out = m.run_pert_model()
     if timings is not None:
         timings.update({k: v for k, v in m.timings.items() if isinstance(v, float)})
+        for k in ("tau_init_s", "tau_init_g"):          # the initialiser's cells: the rank's own
+            timings[k + "_cells"] = float(m.timings.get(k, {}).get("cells", -1))
     return out
 
 
@@ -79,10 +81,14 @@ def test_run_pert_model_two_ranks_match_single_rank(tmp_path):
     tm1 = {}
     cn_s, supp_s, cn_g, supp_g = _fit(timings=tm1)
     from tests._bounds import write_report
-    keys = ("helper_guess_times_s", "helper_guess_times_g", "helper_priors", "total")
+    keys = ("helper_guess_times_s", "helper_guess_times_g", "helper_priors", "total", "tau_init_s_cells",
+            "tau_init_g_cells")
     write_report("api_two_ranks_timings", {"one_rank": {k: tm1.get(k) for k in keys},
                                            "rank0": {k: r[0]["timings"].get(k) for k in keys},
                                            "rank1": {k: r[1]["timings"].get(k) for k in keys}})
+    # each rank initialised tau for its own cells only (pert_model: per-rank host work)
+    for i in range(2):
+        assert r[i]["timings"]["tau_init_s_cells"] == 35 and r[i]["timings"]["tau_init_g_cells"] == 30
     cols = ["model_cn_state", "model_rep_state", "model_tau", "model_u", "model_rho"]
     for i in range(2):
         for name, ref in (("s", cn_s), ("g", cn_g)):

@@ -79,6 +79,32 @@ def test_argument_validation_without_launch(nat):
     assert rc == 1                      # PERT_E_ARG (null pointers)
 
 
+def test_comm_loads_rccl_and_refuses_bad_arguments(nat):
+    """pert_comm_load finds the RCCL this process already uses (torch's) and resolves its
+    symbols; a unique id is made without a GPU; the sharded loop entry points refuse a null
+    communicator and a grad_local aliasing grad_shared before any launch."""
+    import ctypes
+    from scdna_replication_tools_amd.engine import rccl_path
+    lib = nat.lib_nogil()
+    assert lib.pert_comm_load(b"/nonexistent/librccl.so") in (0, 5)   # 0 once an earlier call loaded it
+    assert lib.pert_comm_load(rccl_path().encode()) == 0
+    uid = (ctypes.c_uint8 * 128)()
+    assert lib.pert_comm_unique_id(uid, 128) == 0 and any(bytes(uid))
+    assert lib.pert_comm_unique_id(uid, 64) == 1
+    assert lib.pert_comm_allreduce_sum_f64(None, None, None, 1, None) == 1
+    assert lib.pert_comm_destroy(None) == 0
+    pr = nat.PertProblem(kind=2, L=10, N=10, P=13, K1=5, n_libs=1, ldn=256)
+    st = nat.PertState()
+    hp = nat.PertAdamHparams()
+    f = (ctypes.c_float * 4)()
+    n = ctypes.c_int32()
+    host = (ctypes.c_double * 8)()
+    assert lib.pert_svi_steps_sharded(ctypes.byref(pr), ctypes.byref(st), ctypes.byref(hp), f, f, 0, 1, 0, None,
+                                      None, None, None) == 1
+    assert lib.pert_svi_run_sharded(ctypes.byref(pr), ctypes.byref(st), ctypes.byref(hp), f, f, 1, 8, 8, 0, None,
+                                    None, host, ctypes.byref(n), None) == 1
+
+
 def test_nb_lgdiff_host_matches_scipy(nat):
     rng = np.random.default_rng(1)
     d = np.concatenate([rng.uniform(1, 8, 2000), np.exp(rng.uniform(np.log(8), np.log(3e4), 4000))]).astype(np.float32)

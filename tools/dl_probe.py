@@ -92,8 +92,23 @@ def main():
         port = s.getsockname()[1]
         s.close()
         cmd = [[sys.executable, __file__, "--child", str(r), "2", str(port)] for r in range(2)]
-    procs = [subprocess.Popen(c, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True) for c in cmd]
-    outs = [p.communicate(timeout=300)[1] for p in procs]
+    # each child's stderr to a file of its own (a pipe read one child at a time would fill up
+    # for the other and stall both ranks inside a collective)
+    out_dir = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out_dir, exist_ok=True)
+    files = [os.path.join(out_dir, "dl_probe_rank{}.log".format(r)) for r in range(len(cmd))]
+    fhs = [open(f, "w") for f in files]
+    procs = [subprocess.Popen(c, env=env, stdout=subprocess.DEVNULL, stderr=fh) for c, fh in zip(cmd, fhs)]
+    t0 = time.time()
+    while any(p.poll() is None for p in procs):
+        time.sleep(5)
+        print("... probe running {:.0f} s".format(time.time() - t0), flush=True)
+        if time.time() - t0 > 240:
+            for p in procs:
+                p.kill()
+    for fh in fhs:
+        fh.close()
+    outs = [open(f, errors="replace").read() for f in files]
     rc = [p.returncode for p in procs]
     for r, text in enumerate(outs):
         rows = parse(text)

@@ -338,6 +338,11 @@ int pert_selftest_enum_cellbin_host(int32_t P, int64_t n, const float* x, const 
                                     const float* S1, const float* z, float log1m_lam,
                                     const float* D, const float* phi, float* E, float* dirv,
                                     float* gD, float* gt, float* gz, int32_t* argmax);
+/* The three-wave pass's per-element arithmetic (enum_online + the tail's logit gradient with
+ * the argmax logit in jmax form) on the host: E and d(E + dirv)/dz. */
+int pert_selftest_enum_online_host(int32_t P, int64_t n, const float* x, const float* em1,
+                                   const float* S1, const float* z, float log1m_lam, const float* D,
+                                   const float* phi, float* E, float* gz);
 
 const char* pert_version(void);
 

@@ -27,7 +27,7 @@ BLOCK = 256
 EXPORTED_SYMBOLS = (
     "pert_make_layout", "pert_workspace_sizes", "pert_auto_bins_per_tile", "pert_enum_pass", "pert_obs_pass",
     "pert_finalize", "pert_adam", "pert_enum_step", "pert_adam_shared", "pert_stream_ceiling", "pert_selftest_nb_lgdiff_host",
-    "pert_selftest_nb_lgdiff_device", "pert_selftest_enum_cellbin_host", "pert_tau_binarize", "pert_svi_steps",
+    "pert_selftest_nb_lgdiff_device", "pert_selftest_enum_cellbin_host", "pert_selftest_enum_online_host", "pert_tau_binarize", "pert_svi_steps",
     "pert_svi_run", "pert_comm_load", "pert_comm_unique_id", "pert_comm_init", "pert_comm_destroy",
     "pert_comm_allreduce_sum_f64", "pert_svi_steps_sharded", "pert_svi_run_sharded", "pert_version",
 )
@@ -181,6 +181,7 @@ def load(path: str, gil: bool = True):
     handle.pert_selftest_nb_lgdiff_device.argtypes = [i64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     handle.pert_selftest_enum_cellbin_host.argtypes = [i32, i64, fp, fp, fp, fp, c_float, fp, fp, fp, fp,
                                                        fp, fp, fp, POINTER(i32)]
+    handle.pert_selftest_enum_online_host.argtypes = [i32, i64, fp, fp, fp, fp, c_float, fp, fp, fp, fp]
     handle.pert_tau_binarize.argtypes = [i32, i32, c_void_p, POINTER(PertTauParams), c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_void_p, c_void_p]
     handle.pert_version.restype = c_char_p
@@ -254,3 +255,17 @@ def selftest_enum_cellbin_host(P, x, em1, S1, z, log1m_lam, D, phi):
                                                 am.ctypes.data_as(POINTER(c_int32))),
           "pert_selftest_enum_cellbin_host")
     return dict(E=E, dirv=dirv, gD=gD, gt=gt, gz=gz, argmax=am)
+
+
+def selftest_enum_online_host(P, x, em1, S1, z, log1m_lam, D, phi):
+    """Host evaluation of the three-wave pass's arithmetic (enum_online + enum_jmax, test-only)."""
+    import numpy as np
+    f = lambda a: np.ascontiguousarray(a, dtype=np.float32)
+    x, em1, S1, z, D, phi = map(f, (x, em1, S1, z, D, phi))
+    n = x.size
+    E = np.empty(n, np.float32)
+    gz = np.empty((n, P), np.float32)
+    check(lib().pert_selftest_enum_online_host(P, n, _fptr(x), _fptr(em1), _fptr(S1), _fptr(z), float(log1m_lam),
+                                               _fptr(D), _fptr(phi), _fptr(E), _fptr(gz)),
+          "pert_selftest_enum_online_host")
+    return dict(E=E, gz=gz)

@@ -2155,6 +2155,33 @@ int selftest_enum_host(int64_t n, const float* x, const float* em1, const float*
   return PERT_OK;
 }
 
+// the three-wave pass's arithmetic on the host: enum_online's forward summary, then the tail's
+// pi-logit gradient as enum3_kernel forms it (enum_jmax for the argmax logit), returned as
+// d(E + dirv)/dz (the sign of enum_tail's gz)
+template <int P>
+int selftest_online_host(int64_t n, const float* x, const float* em1, const float* S1, const float* z,
+                         float log1m_lam, const float* D, const float* phi, float* E, float* gz) {
+  for (int64_t i = 0; i < n; ++i) {
+    float e[P], zz[P];
+    for (int k = 0; k < P; ++k) { e[k] = em1[i * P + k]; zz[k] = z[i * P + k]; }
+    const float xi = x[i];
+    EnumOnline<P> o;
+    enum_online<P, kEnum3Group, true, false>(xi, xi > 0.0f ? 1.0f / xi : 0.0f, zz, log1m_lam, D[i], phi[i], o);
+    E[i] = o.E;
+    int jmax;
+    float om, lpj;
+    enum_jmax<P>(zz, o, jmax, om, lpj);
+    const float S1s = S1[i] + o.sgm;
+    const float tom = S1s * om;
+    for (int k = 0; k < P; ++k) {
+      const float gl = enum_pi(o, zz[k], k) * S1s - e[k] - o.gcm[k];
+      const float gj = ((S1[i] - e[k]) + (o.sgm - o.gcm[k])) - tom;
+      gz[i * P + k] = -(k == jmax ? gj : gl);
+    }
+  }
+  return PERT_OK;
+}
+
 }  // namespace
 
 // ============================================================================ C ABI
@@ -2558,6 +2585,18 @@ int pert_selftest_enum_cellbin_host(int32_t P, int64_t n, const float* x, const 
   switch (P) {
 #define PERT_CASE(PP) \
   case PP: return selftest_enum_host<PP>(n, x, em1, S1, z, log1m_lam, D, phi, E, dirv, gD, gt, gz, amax);
+    PERT_ALL_P_CASES
+#undef PERT_CASE
+    default: return PERT_E_UNSUPPORTED_P;
+  }
+}
+
+int pert_selftest_enum_online_host(int32_t P, int64_t n, const float* x, const float* em1, const float* S1,
+                                   const float* z, float log1m_lam, const float* D, const float* phi, float* E,
+                                   float* gz) {
+  switch (P) {
+#define PERT_CASE(PP) \
+  case PP: return selftest_online_host<PP>(n, x, em1, S1, z, log1m_lam, D, phi, E, gz);
     PERT_ALL_P_CASES
 #undef PERT_CASE
     default: return PERT_E_UNSUPPORTED_P;

@@ -555,9 +555,11 @@ PERT_HD void enum_jmax(const float (&z)[P], const EnumOnline<P>& o, int& jmax, f
     t += (k == jmax) ? 0.0f : e;
     s += (k == jmax) ? 1.0f : e;
   }
-  // 1 - pi_jmax from exp(z_k - m) themselves: t / c, to first order in d
-  const float d = fmaf(m, kLog2e, -o.zmaxS);
-  om = (t * o.inv1t) * fmaf(-d, kLn2, 1.0f);
+  // 1 - pi_jmax = the other states' pi_k summed: t = c S and inv1t = 1 / (c (1 + S)) carry the
+  // same scale c (enum_online's total includes the argmax's 2^d), so t inv1t = S / (1 + S) and
+  // the argmax logit's gradient is minus the sum of the others' (enum_pi gives e_k inv1t), as
+  // in enum_forward (the lpj row sum s, unscaled, is the reference's own)
+  om = t * o.inv1t;
   lpj = ref_log_pi_from_sum(s);
 }
 

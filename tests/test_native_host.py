@@ -218,3 +218,38 @@ def test_argmax_logit_gradient_at_saturation(nat):
     # the per-element form's value on these elements misses the pull
     old = (em1 - torch.softmax(torch.tensor(z), -1).numpy() * S1[:, None])[i, st]
     assert np.abs(old - ref).max() > 50 * 2e-4
+
+
+def test_online_argmax_gradient_is_minus_the_others_sum(nat):
+    """The three-wave pass's arithmetic (enum_online + enum_jmax, run on the host): the argmax
+    logit's gradient is minus the sum of the other logits' gradients (a softmax gradient sums
+    to zero), as in enum_forward -- 1 - pi_jmax is the others' pi summed with the same scaled
+    exponentials and the same 1 / total, with no further correction -- and E equals
+    enum_forward's.  Saturated rows (fp32 pi_argmax rounds to 1) included."""
+    P, n = 13, 20000
+    rng = np.random.default_rng(7)
+    x = rng.integers(50, 300, n).astype(np.float32)
+    st = rng.integers(0, P, n)
+    em1 = np.zeros((n, P), np.float32)
+    em1[np.arange(n), st] = np.float32(1e6 - 1)
+    S1 = em1.sum(1)
+    z = (rng.normal(size=(n, P)) * 0.5).astype(np.float32)
+    z[np.arange(n), st] += rng.uniform(0.0, 63.0, n).astype(np.float32)
+    D = rng.uniform(20, 60, n).astype(np.float32)
+    phi = rng.uniform(0.01, 0.99, n).astype(np.float32)
+    fwd = nat.selftest_enum_cellbin_host(P, x, em1, S1, z, np.log1p(-0.75), D, phi)
+    onl = nat.selftest_enum_online_host(P, x, em1, S1, z, np.log1p(-0.75), D, phi)
+    np.testing.assert_allclose(onl["E"], fwd["E"], rtol=0, atol=2e-6 * float(np.abs(fwd["E"]).max()))
+    i = np.arange(n)
+    eps = float(np.finfo(np.float32).eps)
+    for out in (onl, fwd):
+        g = out["gz"].astype(np.float64)
+        gj = g[i, st]
+        others = g.sum(1) - gj
+        mag = np.abs(g).sum(1) - np.abs(gj)                 # the others' terms, before cancellation
+        ulps = np.abs(gj + others) / (np.abs(others) * eps + 1e-30)
+        ulps_mag = np.abs(gj + others) / (mag * eps + 1e-30)
+        # the residual is the rounding of the others' pi summed two ways (a few ulps); a scale
+        # correction on 1 - pi_jmax alone showed up here as up to ~1,300 ulps (p99 ~22)
+        assert np.percentile(ulps, 99) < 4.0, np.percentile(ulps, 99)
+        assert ulps_mag.max() < 64.0, ulps_mag.max()

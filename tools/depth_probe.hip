@@ -1,0 +1,147 @@
+// Bytes-in-flight probe for the enumerated pass's access pattern (diagnostic, not product code).
+//
+// The step-2 pass streams per 64-cell wave tile and bin: x (256 B) + eta code (128 B) read, and
+// the pi logits z, Adam moments m, v (P x 256 B each) read and written back in place; each wave
+// keeps ONE bin of loads in flight ahead of the bin it works on.  A small shard (1,250 cells, the
+// per-rank work of C4 on 8 GPUs) launches one round of ~2,000 such waves, a 10 k-cell shard keeps
+// ~3,000 resident: if the pattern is latency-bound (Little's law) the small shard's ceiling sits
+// below the large one's.  This probe runs the same streams with no arithmetic at lookahead depth
+// D = 1..3 bins (register buffers) and at a chosen number of resident waves per CU (LDS padding),
+// so the ceiling can be read as a function of bytes in flight.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++20 tools/depth_probe.hip -o tools/depth_probe
+//   ./depth_probe [cells=1250] [bins=5451] [LT=54] [waves_per_cu=12] [iters=20]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                       \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess) {                                                         \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));     \
+      exit(1);                                                                      \
+    }                                                                               \
+  } while (0)
+
+constexpr int P = 13;
+
+template <int D>
+__global__ void __launch_bounds__(64) depth_stream(const float* __restrict__ x, const uint16_t* __restrict__ code,
+                                                   float* z, float* m, float* v, int L, int ldn, int LT, float* sink) {
+  extern __shared__ float pad[];                  // occupancy cap: dynamic LDS per workgroup
+  const int lane = threadIdx.x;
+  if (lane == 0 && LT < 0) pad[0] = 0.0f;
+  const int wt = blockIdx.x, bt = blockIdx.y;
+  const int l0 = bt * LT, l1 = min(L, l0 + LT);
+  const size_t t0 = ((size_t)wt * L) * P * 64 + lane;
+  float zr[D][P], mr[D][P], vr[D][P], xr[D];
+  uint32_t cr[D];
+  float acc = 0.0f;
+  auto load = [&](auto dd, int l) {
+    constexpr int d = decltype(dd)::value;
+    const size_t o = t0 + (size_t)l * P * 64;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      zr[d][k] = __builtin_nontemporal_load(z + o + k * 64);
+      mr[d][k] = __builtin_nontemporal_load(m + o + k * 64);
+      vr[d][k] = __builtin_nontemporal_load(v + o + k * 64);
+    }
+    xr[d] = x[(size_t)l * ldn + wt * 64 + lane];
+    cr[d] = code[(size_t)l * ldn + wt * 64 + lane];
+  };
+  auto each = [&](auto f) {
+    [&]<int... I>(std::integer_sequence<int, I...>) { (f(std::integral_constant<int, I>{}), ...); }
+    (std::make_integer_sequence<int, D>{});
+  };
+  each([&](auto dd) {
+    if (l0 + decltype(dd)::value < l1) load(dd, l0 + decltype(dd)::value);
+  });
+  for (int l = l0; l < l1; l += D) {
+    each([&](auto dd) {
+      constexpr int d = decltype(dd)::value;
+      const int lc = l + d;
+      if (lc < l1) {
+        float zc[P], mc[P], vc[P];
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+          zc[k] = zr[d][k];
+          mc[k] = mr[d][k];
+          vc[k] = vr[d][k];
+        }
+        acc += xr[d] + (float)cr[d];
+        if (lc + D < l1) load(dd, lc + D);
+        const size_t o = t0 + (size_t)lc * P * 64;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+          asm volatile("" : "+v"(zc[k]), "+v"(mc[k]), "+v"(vc[k]));
+          __builtin_nontemporal_store(zc[k], z + o + k * 64);
+          __builtin_nontemporal_store(mc[k], m + o + k * 64);
+          __builtin_nontemporal_store(vc[k], v + o + k * 64);
+        }
+      }
+    });
+  }
+  if (acc == 12345.678f) sink[0] = acc;
+}
+
+template <class F>
+static float time_ms(F f, int iters) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  f();
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < iters; ++i) f();
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / iters;
+}
+
+int main(int argc, char** argv) {
+  const int N = argc > 1 ? atoi(argv[1]) : 1250;
+  const int L = argc > 2 ? atoi(argv[2]) : 5451;
+  const int LT = argc > 3 ? atoi(argv[3]) : 54;
+  const int wpc = argc > 4 ? atoi(argv[4]) : 12;
+  const int iters = argc > 5 ? atoi(argv[5]) : 20;
+  if (N <= 0 || L <= 0 || LT <= 0 || wpc <= 0 || wpc > 32) return 2;
+  const int ldn = (N + 255) / 256 * 256;
+  const int nwt = (N + 63) / 64;
+  const size_t nz = (size_t)(ldn / 64) * L * P * 64;
+  float *z, *m, *v, *x, *sink;
+  uint16_t* code;
+  CK(hipMalloc(&z, nz * 4));
+  CK(hipMalloc(&m, nz * 4));
+  CK(hipMalloc(&v, nz * 4));
+  CK(hipMalloc(&x, (size_t)L * ldn * 4));
+  CK(hipMalloc(&code, (size_t)L * ldn * 2));
+  CK(hipMalloc(&sink, 64));
+  CK(hipMemset(z, 0, nz * 4));
+  CK(hipMemset(m, 0, nz * 4));
+  CK(hipMemset(v, 0, nz * 4));
+  CK(hipMemset(x, 0, (size_t)L * ldn * 4));
+  CK(hipMemset(code, 0, (size_t)L * ldn * 2));
+  const double bytes = (double)nwt * 64 * L * (6.0 + 24.0 * P);   // the launched tiles' bytes
+  const int nbt = (L + LT - 1) / LT;
+  const dim3 grid(nwt, nbt);
+  const size_t lds = (size_t)(160 * 1024) / wpc - 256;
+  int dev = 0, ncu = 0;
+  CK(hipGetDevice(&dev));
+  CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  int occ[3] = {0, 0, 0};
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[0], depth_stream<1>, 64, lds));
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1], depth_stream<2>, 64, lds));
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[2], depth_stream<3>, 64, lds));
+  const float t1 = time_ms([&] { depth_stream<1><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, sink); }, iters);
+  const float t2 = time_ms([&] { depth_stream<2><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, sink); }, iters);
+  const float t3 = time_ms([&] { depth_stream<3><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, sink); }, iters);
+  printf("cells %d bins %d LT %d tiles %d (%.2f rounds of %d x %d slots): depth1 %.4f ms %.3f TB/s | depth2 %.4f ms "
+         "%.3f TB/s | depth3 %.4f ms %.3f TB/s (occupancy %d/%d/%d)\n",
+         N, L, LT, nwt * nbt, (double)nwt * nbt / ((double)ncu * occ[0]), ncu, occ[0], t1, bytes / t1 / 1e9, t2,
+         bytes / t2 / 1e9, t3, bytes / t3 / 1e9, occ[0], occ[1], occ[2]);
+  return 0;
+}

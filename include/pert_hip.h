@@ -234,15 +234,17 @@ int pert_svi_steps(const pert_problem* prob, pert_state* st, const pert_adam_hpa
  * n_iter iterations queued in chunks of `chunk` (pert_svi_steps, step_size / inv_bc2_sqrt hold
  * all n_iter entries), each chunk followed by a copy of its loss records into host_rec (pinned
  * host memory, [n_iter][2] doubles) and an event; at most `depth` chunks are in flight, and
- * queueing ends once a copied record shows the stop.  Returns after the stream has drained,
+ * queueing ends once a copied record shows the stop.  pass_events: NULL, or 2 n_iter
+ * caller-created events (NULL entries skipped) recorded around iteration i's pass as in
+ * pert_svi_steps.  Returns after the stream has drained,
  * with *n_launched = the iterations queued (loop_ctl[0] holds the stopping iteration).  One
  * call per fit, so a binding that releases its interpreter lock around it leaves the host
  * thread free for the rest of the program for the whole fit.  Replaces the loop of
  * pert_model.py:742-758 / :800-816 / :867-883. */
 int pert_svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
                  const float* step_size, const float* inv_bc2_sqrt, int32_t n_iter, int32_t chunk,
-                 int32_t depth, int32_t one_launch, double* host_rec, int32_t* n_launched,
-                 hipStream_t stream);
+                 int32_t depth, int32_t one_launch, hipEvent_t* pass_events, double* host_rec,
+                 int32_t* n_launched, hipStream_t stream);
 
 /* ---- Sharded fits: cells split over ranks, one process per GPU.
  * The shared block's gradient [0, n_shared) and the loss (slot n_shared) are summed across
@@ -277,7 +279,7 @@ int pert_svi_steps_sharded(const pert_problem* prob, pert_state* st, const pert_
 int pert_svi_run_sharded(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
                          const float* step_size, const float* inv_bc2_sqrt, int32_t n_iter, int32_t chunk,
                          int32_t depth, int32_t one_launch, pert_comm* comm, double* grad_local,
-                         double* host_rec, int32_t* n_launched, hipStream_t stream);
+                         hipEvent_t* pass_events, double* host_rec, int32_t* n_launched, hipStream_t stream);
 
 /* Diagnostic (bench.py): the HBM streams of pert_enum_pass(PERT_MODE_STEP) -- x, eta code,
  * z/m/v read and written back unchanged, same grid and tile length -- with no arithmetic.

@@ -166,7 +166,7 @@ def load(path: str, gil: bool = True):
     handle.pert_svi_steps.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams), fp, fp,
                                       i32, i32, i32, c_void_p, c_void_p]
     handle.pert_svi_run.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams), fp, fp,
-                                    i32, i32, i32, i32, c_void_p, POINTER(i32), c_void_p]
+                                    i32, i32, i32, i32, c_void_p, c_void_p, POINTER(i32), c_void_p]
     handle.pert_comm_load.argtypes = [c_char_p]
     handle.pert_comm_unique_id.argtypes = [c_void_p, i32]
     handle.pert_comm_init.argtypes = [c_void_p, i32, i32, i32, POINTER(c_void_p)]
@@ -175,8 +175,8 @@ def load(path: str, gil: bool = True):
     handle.pert_svi_steps_sharded.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams), fp,
                                               fp, i32, i32, i32, c_void_p, c_void_p, c_void_p, c_void_p]
     handle.pert_svi_run_sharded.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams), fp,
-                                            fp, i32, i32, i32, i32, c_void_p, c_void_p, c_void_p, POINTER(i32),
-                                            c_void_p]
+                                            fp, i32, i32, i32, i32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                            POINTER(i32), c_void_p]
     handle.pert_selftest_nb_lgdiff_host.argtypes = [i64, fp, fp, fp, fp]
     handle.pert_selftest_nb_lgdiff_device.argtypes = [i64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     handle.pert_selftest_enum_cellbin_host.argtypes = [i32, i64, fp, fp, fp, fp, c_float, fp, fp, fp, fp,

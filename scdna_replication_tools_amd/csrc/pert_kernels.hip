@@ -2469,7 +2469,8 @@ int svi_steps(const pert_problem* prob, pert_state* st, const pert_adam_hparams*
 
 int svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp, const float* step_size,
             const float* inv_bc2_sqrt, int32_t n_iter, int32_t chunk, int32_t depth, int32_t one_launch,
-            pert_comm* comm, double* grad_local, double* host_rec, int32_t* n_launched, hipStream_t stream) {
+            pert_comm* comm, double* grad_local, hipEvent_t* pass_events, double* host_rec, int32_t* n_launched,
+            hipStream_t stream) {
   if (!st || !st->loop_ctl || !st->loop_rec || !host_rec || !n_launched || n_iter < 0 || chunk < 1 || depth < 1)
     return PERT_E_ARG;
   *n_launched = 0;
@@ -2497,8 +2498,8 @@ int svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hparams* h
     if (c - waited >= ring - 1) look(waited++);          // the ring's oldest chunk is done
     if (stop_seen || rc != PERT_OK) break;
     const int j0 = c * chunk, n = (j0 + chunk < n_iter ? j0 + chunk : n_iter) - j0;
-    rc = svi_steps(prob, st, hp, step_size + j0, inv_bc2_sqrt + j0, j0, n, one_launch, comm, grad_local, nullptr,
-                   stream);
+    rc = svi_steps(prob, st, hp, step_size + j0, inv_bc2_sqrt + j0, j0, n, one_launch, comm, grad_local,
+                   pass_events ? pass_events + 2 * j0 : nullptr, stream);
     if (rc == PERT_OK)
       rc = hip_status(hipMemcpyAsync(host_rec + 2 * j0, st->loop_rec + 2 * j0, sizeof(double) * 2 * n,
                                      hipMemcpyDeviceToHost, stream));
@@ -2523,9 +2524,9 @@ int pert_svi_steps(const pert_problem* prob, pert_state* st, const pert_adam_hpa
 
 int pert_svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp, const float* step_size,
                  const float* inv_bc2_sqrt, int32_t n_iter, int32_t chunk, int32_t depth, int32_t one_launch,
-                 double* host_rec, int32_t* n_launched, hipStream_t stream) {
-  return svi_run(prob, st, hp, step_size, inv_bc2_sqrt, n_iter, chunk, depth, one_launch, nullptr, nullptr, host_rec,
-                 n_launched, stream);
+                 hipEvent_t* pass_events, double* host_rec, int32_t* n_launched, hipStream_t stream) {
+  return svi_run(prob, st, hp, step_size, inv_bc2_sqrt, n_iter, chunk, depth, one_launch, nullptr, nullptr,
+                 pass_events, host_rec, n_launched, stream);
 }
 
 int pert_svi_steps_sharded(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
@@ -2538,11 +2539,11 @@ int pert_svi_steps_sharded(const pert_problem* prob, pert_state* st, const pert_
 
 int pert_svi_run_sharded(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp,
                          const float* step_size, const float* inv_bc2_sqrt, int32_t n_iter, int32_t chunk,
-                         int32_t depth, int32_t one_launch, pert_comm* comm, double* grad_local, double* host_rec,
-                         int32_t* n_launched, hipStream_t stream) {
+                         int32_t depth, int32_t one_launch, pert_comm* comm, double* grad_local,
+                         hipEvent_t* pass_events, double* host_rec, int32_t* n_launched, hipStream_t stream) {
   if (!comm) return PERT_E_ARG;
-  return svi_run(prob, st, hp, step_size, inv_bc2_sqrt, n_iter, chunk, depth, one_launch, comm, grad_local, host_rec,
-                 n_launched, stream);
+  return svi_run(prob, st, hp, step_size, inv_bc2_sqrt, n_iter, chunk, depth, one_launch, comm, grad_local,
+                 pass_events, host_rec, n_launched, stream);
 }
 
 int pert_stream_ceiling(const pert_problem* prob, pert_state* st, hipStream_t stream) {

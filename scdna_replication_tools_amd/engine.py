@@ -752,6 +752,16 @@ class PertShard:
             self._ctl_init = torch.tensor([-1, 0], dtype=torch.int32, device=self.device)
         return self._loop_bufs
 
+    def _timing_event(self):
+        """A timing event from the pool reserve_svi fills (created and recorded once, so its HIP
+        event exists), or a new one."""
+        pool = self.__dict__.setdefault("_event_pool", [])
+        if pool:
+            return pool.pop()
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()                                  # creates the HIP event behind it
+        return e
+
     def reserve_svi(self, n: int) -> None:
         """Set up everything a run_svi(n) from the current step allocates or computes on the
         host -- its loop buffers and, for step 1, the canonical pi trajectory -- ahead of the
@@ -760,6 +770,13 @@ class PertShard:
         self._loop_buffers(int(n))
         if self.pi_block is not None:
             self.pi_block._cache(self.t + int(n) + 1)
+        if self.pass_events is not None:            # the timing events a run_svi(n) will record
+            need = 2 * len(range(0, int(n), max(1, self.pass_event_stride)))
+            pool = self.__dict__.setdefault("_event_pool", [])
+            while len(pool) < need:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record()
+                pool.append(e)
 
     def run_svi(self, max_iter: int, min_iter: int, rel_tol: float, chunk: int = 8, depth: int = 8):
         """The SVI loop of pert_model.py:742-758 (:800-816, :867-883) without a per-step host
@@ -790,21 +807,29 @@ class PertShard:
         # one rank, or ranks joined by a pert_comm: the whole loop is ONE C call (pert_svi_run /
         # pert_svi_run_sharded, the all-reduce queued by the library) that releases the GIL for
         # the fit's duration -- a helper thread's Python work never delays the queueing of steps;
-        # with per-pass timing events (pass_events, bench.py) a chunk of iterations per C call
-        # (pert_svi_steps[_sharded], the events recorded around each pass); sharded over another
-        # process group (gloo), per iteration from Python (torch.distributed's all-reduce sits
-        # between the reductions and Adam)
+        # per-pass timing events (pass_events, bench.py) are recorded by that call around the
+        # passes of every pass_event_stride-th iteration.  Sharded over another process group
+        # (gloo): per iteration from Python (torch.distributed's all-reduce sits between the
+        # reductions and Adam)
         native_comm = self.comm is not None and self.allreduce == self.comm.allreduce
-        chunked = (self.allreduce is None or native_comm) and self._lib_chunk is not None
+        native = (self.allreduce is None or native_comm) and self._lib_chunk is not None
         shard_args = (self.comm.handle, _ptr(self.grad_local)) if native_comm else ()
         b1, b2 = self.betas
         launched = 0
         pending = []
         try:
-            if chunked and self.pass_events is None:
+            if native:
                 ts = range(t0 + 1, t0 + n + 1)
                 ss = np.array([self.lr / (1.0 - b1 ** t) for t in ts], dtype=F32)         # as _set_hparams
                 ib = np.array([1.0 / math.sqrt(1.0 - b2 ** t) for t in ts], dtype=F32)
+                evp, sampled = None, []
+                if self.pass_events is not None:
+                    ptrs = [None] * (2 * n)
+                    for i in range(0, n, max(1, self.pass_event_stride)):
+                        e0, e1 = self._timing_event(), self._timing_event()
+                        ptrs[2 * i], ptrs[2 * i + 1] = e0.cuda_event, e1.cuda_event
+                        sampled.append((i, e0, e1))
+                    evp = (ctypes.c_void_p * len(ptrs))(*ptrs)
                 nl = ctypes.c_int32(0)
                 fn = self._lib_chunk.pert_svi_run_sharded if native_comm else self._lib_chunk.pert_svi_run
                 with self._dev():
@@ -812,39 +837,17 @@ class PertShard:
                         ctypes.byref(self._prob), ctypes.byref(st), ctypes.byref(self._hp),
                         ss.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
                         ib.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n, chunk, depth,
-                        1 if self.fused else 0, *shard_args, host.data_ptr(), ctypes.byref(nl), self._stream()),
-                        "pert_svi_run")
+                        1 if self.fused else 0, *shard_args, evp, host.data_ptr(), ctypes.byref(nl),
+                        self._stream()), "pert_svi_run")
                 launched = int(nl.value)
-                n = 0                              # nothing left for the chunk loop below
+                if self.pass_events is not None:       # (iterations never queued recorded nothing)
+                    self.pass_events.extend((e0, e1) for i, e0, e1 in sampled if i < launched)
+                n = 0                              # nothing left for the per-iteration loop below
             for j0 in range(0, n, chunk):
                 j1 = min(n, j0 + chunk)
-                if chunked:
-                    ts = range(t0 + j0 + 1, t0 + j1 + 1)
-                    ss = np.array([self.lr / (1.0 - b1 ** t) for t in ts], dtype=F32)     # as _set_hparams
-                    ib = np.array([1.0 / math.sqrt(1.0 - b2 ** t) for t in ts], dtype=F32)
-                    evp = None
-                    if self.pass_events is not None:
-                        # events around the passes of every pass_event_stride-th iteration
-                        ptrs = [None] * (2 * (j1 - j0))
-                        for i in range(j0, j1):
-                            if i % self.pass_event_stride == 0:
-                                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                                e0.record()                # creates the HIP events behind them
-                                e1.record()
-                                ptrs[2 * (i - j0)], ptrs[2 * (i - j0) + 1] = e0.cuda_event, e1.cuda_event
-                                self.pass_events.append((e0, e1))
-                        evp = (ctypes.c_void_p * len(ptrs))(*ptrs)
-                    fn = self._lib_chunk.pert_svi_steps_sharded if native_comm else self._lib_chunk.pert_svi_steps
-                    with self._dev():
-                        nat.check(fn(
-                            ctypes.byref(self._prob), ctypes.byref(st), ctypes.byref(self._hp),
-                            ss.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
-                            ib.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), j0, j1 - j0, 1 if self.fused else 0,
-                            *shard_args, evp, self._stream()), "pert_svi_steps")
-                else:
-                    for i in range(j0, j1):
-                        st.step = i
-                        self._launch_step(t0 + i + 1)
+                for i in range(j0, j1):
+                    st.step = i
+                    self._launch_step(t0 + i + 1)
                 launched = j1
                 host[j0:j1].copy_(rec[j0:j1], non_blocking=True)
                 ev = torch.cuda.Event()

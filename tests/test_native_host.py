@@ -102,7 +102,7 @@ def test_comm_loads_rccl_and_refuses_bad_arguments(nat):
     assert lib.pert_svi_steps_sharded(ctypes.byref(pr), ctypes.byref(st), ctypes.byref(hp), f, f, 0, 1, 0, None,
                                       None, None, None) == 1
     assert lib.pert_svi_run_sharded(ctypes.byref(pr), ctypes.byref(st), ctypes.byref(hp), f, f, 1, 8, 8, 0, None,
-                                    None, host, ctypes.byref(n), None) == 1
+                                    None, None, host, ctypes.byref(n), None) == 1
 
 
 def test_nb_lgdiff_host_matches_scipy(nat):

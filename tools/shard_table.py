@@ -1,0 +1,41 @@
+"""One-lease strong-scaling table from bench.py lines.
+
+Reads the JSON lines tools/r05d.sh collected (each a bench.py run: the 10 k-cell C4 step on one
+rank, and the per-rank shard of an N-GPU run -- 10 k / N cells -- with the library's RCCL
+all-reduce at world 1) and prints, per repetition, the projected N-GPU efficiency
+T(10 k) / (N x T(10 k / N)) from the timed steps (HIP events on every 5th pass) and from the
+same steps without events (the production loop).
+
+    python tools/shard_table.py gpurun_out/r05d_shards.jsonl
+"""
+import json
+import sys
+
+
+def main(path):
+    rows = [json.loads(l) for l in open(path) if l.strip().startswith("{")]
+    reps = {}
+    for r in rows:
+        key = (r.get("_rep"), r["config"]["cells"], bool(r.get("_fused")))
+        reps[key] = r
+    for rep in sorted({k[0] for k in reps}):
+        base = reps.get((rep, 10000, False))
+        if base is None:
+            continue
+        t_ev, t_plain = base["ms_per_step"], base.get("ms_per_step_no_events", base["ms_per_step"])
+        print("rep {}: 10,000 cells {:.4f} ms/step (no events {:.4f}), pass {:.4f} ms, ceiling {:.4f} ms".format(
+            rep, t_ev, t_plain, base["roofline"]["kernel_ms"], base["roofline"]["pattern_ceiling"]["ms"]))
+        for (rp, cells, fused), r in sorted(reps.items()):
+            if rp != rep or cells == 10000:
+                continue
+            n = round(10000 / cells)
+            s_ev, s_plain = r["ms_per_step"], r.get("ms_per_step_no_events", r["ms_per_step"])
+            k, c = r["roofline"]["kernel_ms"], r["roofline"]["pattern_ceiling"]["ms"]
+            print("  N={} shard {:5d} cells{}: {:.4f} ms/step (no events {:.4f}), pass {:.4f} ms = {:.3f} of its "
+                  "ceiling {:.4f}; efficiency {:.1%} (no events {:.1%}); allreduce: {}".format(
+                      n, cells, " fused" if fused else "", s_ev, s_plain, k, c / k, c, t_ev / (n * s_ev),
+                      t_plain / (n * s_plain), r["config"]["allreduce"][:40]))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

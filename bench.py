@@ -293,7 +293,7 @@ def main():
                     help="CN prior of the step-2 fit: g1_clones (the tutorial's; one code per clone state) or "
                          "g1_composite (the reference's default; the product's composite code book, many rows)")
     ap.add_argument("--event-stride", type=int, default=5,
-                    help="HIP events around the pass of every k-th timed step (1: every step)")
+                    help="HIP events around the pass of every k-th step of the pass-timing run (1: every step)")
     ap.add_argument("--comm", default="auto", choices=["auto", "rccl", "torch"],
                     help="cross-rank sum of the shared block: 'rccl' = the library's own RCCL communicator "
                          "(pert_comm, queued inside the C loop; the default on N > 1 over nccl, and at N = 1 "
@@ -404,10 +404,12 @@ def main():
         shard.run_svi(args.warmup, min_iter=10 ** 9, rel_tol=0.0)
     # the loop's buffers (and step 1's canonical pi trajectory) set up before the timed region,
     # as run_pert_model has them ready before a fit starts
-    # 0: no events in the timed region (the pass time then comes from 10 instrumented steps after it)
-    shard.pass_events = [] if args.event_stride > 0 else None
-    shard.pass_event_stride = max(1, args.event_stride)
-    shard.reserve_svi(args.steps)                     # (also creates the timing events)
+    # The value's region is the production loop with no timing events (one C call, pert_svi_run):
+    # a HIP timing event on the stream costs the step ~50 us (r05d: 0.497 vs 0.520 ms/step at
+    # 1,250 cells with events around every 5th pass).  The pass durations come from the same K
+    # steps run again right after it, with events around every event_stride-th pass.
+    shard.pass_events = None
+    shard.reserve_svi(args.steps)
     if pg is not None:
         pg.barrier()
     torch.cuda.synchronize()
@@ -419,35 +421,28 @@ def main():
     if pg is not None:
         pg.barrier()
     dt = time.perf_counter() - t0
-    dt_plain = None
-    if shard.pass_events is None:
-        shard.pass_events = []
-        shard.run_svi(10, min_iter=10 ** 9, rel_tol=0.0)
-    else:
-        # the same K steps again on the production host path (no events: one C call for the
-        # whole loop), as a cross-check of the timed region's host path
-        events, shard.pass_events = shard.pass_events, None
-        shard.reserve_svi(args.steps)
-        if pg is not None:
-            pg.barrier()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        shard.run_svi(args.steps, min_iter=10 ** 9, rel_tol=0.0)
-        torch.cuda.synchronize()
-        if pg is not None:
-            pg.barrier()
-        dt_plain = time.perf_counter() - t1
-        shard.pass_events = events
+    # the pass-timing run: the next K steps, HIP events around every event_stride-th pass
+    shard.pass_events = []
+    shard.pass_event_stride = max(1, args.event_stride)
+    shard.reserve_svi(args.steps)                     # (also creates the timing events)
+    if pg is not None:
+        pg.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    shard.run_svi(args.steps, min_iter=10 ** 9, rel_tol=0.0)
+    torch.cuda.synchronize()
+    if pg is not None:
+        pg.barrier()
+    dt_ev = time.perf_counter() - t1
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in shard.pass_events]))
     shard.pass_events = None
     # after the timed region: the same shard's HBM streams with no arithmetic (the pattern's
     # ceiling on this device, this lease) -- pert_stream_ceiling leaves the state unchanged
     ceil_ms = shard.stream_ceiling_ms() if args.fit != "step1" else None
-    t = torch.tensor([dt, kern_ms, dt_plain if dt_plain is not None else -1.0], dtype=torch.float64, device=device)
+    t = torch.tensor([dt, kern_ms, dt_ev], dtype=torch.float64, device=device)
     if pg is not None:
         pg.all_reduce(t, op=pg.ReduceOp.MAX)
-    dt, kern_ms_max = float(t[0]), float(t[1])
-    dt_plain = float(t[2]) if dt_plain is not None else None
+    dt, kern_ms_max, dt_ev = float(t[0]), float(t[1]), float(t[2])
 
     if rank == 0:
         cellbins_total = L * n_total * (2 if args.fit == "step1" else 1)
@@ -480,10 +475,8 @@ def main():
             "config": {"workload": desc, "config": args.config, "cells": n_total, "bins": L, "P": P,
                        "K": K, "cn_prior": prior_desc, "parallelism": "cell-sharded x{}".format(world),
                        "bins_per_tile": shard.bins_per_tile, "fit": args.fit, "allreduce": comm_desc,
-                       "timed_loop": ("pert_svi_run{}: the whole loop in one GIL-free C call{}".format(
-                                          "_sharded" if comm is not None else "",
-                                          ", HIP events around every {}th pass".format(args.event_stride)
-                                          if args.event_stride > 0 else "")
+                       "timed_loop": ("pert_svi_run{}: the whole loop in one GIL-free C call, no timing "
+                                      "events".format("_sharded" if comm is not None else "")
                                       if comm is not None or allreduce is None
                                       else "per-iteration launches from Python")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -492,18 +485,17 @@ def main():
                                     "enum3_kernel<13, STEP, 5>" if args.variant == 3 else
                                     "enum_dma_kernel<13, STEP, 5>"),
                          "kernel_ms": kern_ms,
-                         "kernel_ms_events": ("HIP events around every pass of the timed steps" if args.event_stride == 1
-                                              else "HIP events around every {}th pass of the timed steps".format(
-                                                  args.event_stride) if args.event_stride > 1
-                                              else "HIP events around 10 passes after the timed region"),
+                         "kernel_ms_events": ("HIP events on the pass's stream around every {} pass of the K steps "
+                                              "run right after the timed region (ms_per_step_evented: their wall "
+                                              "time; events in the value's region would cost ~50 us each)".format(
+                                                  "" if args.event_stride <= 1 else "{}th".format(args.event_stride))),
                          "bytes_per_cellbin": bpc,
                          # PMC (profiles/pmc_traffic.json, tools/profile.sh): VALU issue fraction of
                          # the same kernel -- the other roofline, not the binding one here
                          "valu_issue_frac": (valu or {}).get("issue_frac")},
             "loss_first": losses[0], "loss_last": losses[-1],
         }
-        if dt_plain is not None:
-            rec["ms_per_step_no_events"] = dt_plain / args.steps * 1e3
+        rec["ms_per_step_evented"] = dt_ev / args.steps * 1e3
         if ceil_ms is not None:
             rec["roofline"]["pattern_ceiling"] = {
                 "ms": ceil_ms, "GB/s": bpc * local_cb / (ceil_ms * 1e-3) / 1e9,

@@ -10,7 +10,9 @@
 // so the ceiling can be read as a function of bytes in flight.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++20 tools/depth_probe.hip -o tools/depth_probe
-//   ./depth_probe [cells=1250] [bins=5451] [LT=54] [waves_per_cu=12] [iters=20]
+//   ./depth_probe [cells=1250] [bins=5451] [LT=54] [waves_per_cu=12] [iters=20] [spread=1] [swap=0]
+// spread: cell tiles placed spread x a tile apart (the footprint of a spread x larger shard);
+// swap: blockIdx.x walks the bin tiles instead of the cell tiles.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -29,13 +31,14 @@ constexpr int P = 13;
 
 template <int D>
 __global__ void __launch_bounds__(64) depth_stream(const float* __restrict__ x, const uint16_t* __restrict__ code,
-                                                   float* z, float* m, float* v, int L, int ldn, int LT, float* sink) {
+                                                   float* z, float* m, float* v, int L, int ldn, int LT, int spread,
+                                                   int swap, float* sink) {
   extern __shared__ float pad[];                  // occupancy cap: dynamic LDS per workgroup
   const int lane = threadIdx.x;
   if (lane == 0 && LT < 0) pad[0] = 0.0f;
-  const int wt = blockIdx.x, bt = blockIdx.y;
+  const int wt = swap ? blockIdx.y : blockIdx.x, bt = swap ? blockIdx.x : blockIdx.y;
   const int l0 = bt * LT, l1 = min(L, l0 + LT);
-  const size_t t0 = ((size_t)wt * L) * P * 64 + lane;
+  const size_t t0 = ((size_t)wt * spread * L) * P * 64 + lane;     // spread: tiles apart by spread x a tile
   float zr[D][P], mr[D][P], vr[D][P], xr[D];
   uint32_t cr[D];
   float acc = 0.0f;
@@ -108,10 +111,12 @@ int main(int argc, char** argv) {
   const int LT = argc > 3 ? atoi(argv[3]) : 54;
   const int wpc = argc > 4 ? atoi(argv[4]) : 12;
   const int iters = argc > 5 ? atoi(argv[5]) : 20;
-  if (N <= 0 || L <= 0 || LT <= 0 || wpc <= 0 || wpc > 32) return 2;
+  const int spread = argc > 6 ? atoi(argv[6]) : 1;
+  const int swap = argc > 7 ? atoi(argv[7]) : 0;
+  if (N <= 0 || L <= 0 || LT <= 0 || wpc <= 0 || wpc > 32 || spread < 1 || spread > 16) return 2;
   const int ldn = (N + 255) / 256 * 256;
   const int nwt = (N + 63) / 64;
-  const size_t nz = (size_t)(ldn / 64) * L * P * 64;
+  const size_t nz = (size_t)(ldn / 64) * spread * L * P * 64;
   float *z, *m, *v, *x, *sink;
   uint16_t* code;
   CK(hipMalloc(&z, nz * 4));
@@ -127,7 +132,7 @@ int main(int argc, char** argv) {
   CK(hipMemset(code, 0, (size_t)L * ldn * 2));
   const double bytes = (double)nwt * 64 * L * (6.0 + 24.0 * P);   // the launched tiles' bytes
   const int nbt = (L + LT - 1) / LT;
-  const dim3 grid(nwt, nbt);
+  const dim3 grid(swap ? nbt : nwt, swap ? nwt : nbt);
   const size_t lds = (size_t)(160 * 1024) / wpc - 256;
   int dev = 0, ncu = 0;
   CK(hipGetDevice(&dev));
@@ -136,12 +141,12 @@ int main(int argc, char** argv) {
   CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[0], depth_stream<1>, 64, lds));
   CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1], depth_stream<2>, 64, lds));
   CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[2], depth_stream<3>, 64, lds));
-  const float t1 = time_ms([&] { depth_stream<1><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, sink); }, iters);
-  const float t2 = time_ms([&] { depth_stream<2><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, sink); }, iters);
-  const float t3 = time_ms([&] { depth_stream<3><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, sink); }, iters);
-  printf("cells %d bins %d LT %d tiles %d (%.2f rounds of %d x %d slots): depth1 %.4f ms %.3f TB/s | depth2 %.4f ms "
+  const float t1 = time_ms([&] { depth_stream<1><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, sink); }, iters);
+  const float t2 = time_ms([&] { depth_stream<2><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, sink); }, iters);
+  const float t3 = time_ms([&] { depth_stream<3><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, sink); }, iters);
+  printf("spread %d swap %d cells %d bins %d LT %d tiles %d (%.2f rounds of %d x %d slots): depth1 %.4f ms %.3f TB/s | depth2 %.4f ms "
          "%.3f TB/s | depth3 %.4f ms %.3f TB/s (occupancy %d/%d/%d)\n",
-         N, L, LT, nwt * nbt, (double)nwt * nbt / ((double)ncu * occ[0]), ncu, occ[0], t1, bytes / t1 / 1e9, t2,
+         spread, swap, N, L, LT, nwt * nbt, (double)nwt * nbt / ((double)ncu * occ[0]), ncu, occ[0], t1, bytes / t1 / 1e9, t2,
          bytes / t2 / 1e9, t3, bytes / t3 / 1e9, occ[0], occ[1], occ[2]);
   return 0;
 }

@@ -22,14 +22,19 @@ def main(path):
         base = reps.get((rep, 10000, False))
         if base is None:
             continue
-        t_ev, t_plain = base["ms_per_step"], base.get("ms_per_step_no_events", base["ms_per_step"])
+        # (r05d lines: ms_per_step evented, ms_per_step_no_events plain; later: ms_per_step plain,
+        # ms_per_step_evented)
+        ev = lambda r: r.get("ms_per_step_evented", r["ms_per_step"])
+        plain = lambda r: r["ms_per_step"] if "ms_per_step_evented" in r else r.get("ms_per_step_no_events",
+                                                                                    r["ms_per_step"])
+        t_ev, t_plain = ev(base), plain(base)
         print("rep {}: 10,000 cells {:.4f} ms/step (no events {:.4f}), pass {:.4f} ms, ceiling {:.4f} ms".format(
             rep, t_ev, t_plain, base["roofline"]["kernel_ms"], base["roofline"]["pattern_ceiling"]["ms"]))
         for (rp, cells, fused), r in sorted(reps.items()):
             if rp != rep or cells == 10000:
                 continue
             n = round(10000 / cells)
-            s_ev, s_plain = r["ms_per_step"], r.get("ms_per_step_no_events", r["ms_per_step"])
+            s_ev, s_plain = ev(r), plain(r)
             k, c = r["roofline"]["kernel_ms"], r["roofline"]["pattern_ceiling"]["ms"]
             print("  N={} shard {:5d} cells{}: {:.4f} ms/step (no events {:.4f}), pass {:.4f} ms = {:.3f} of its "
                   "ceiling {:.4f}; efficiency {:.1%} (no events {:.1%}); allreduce: {}".format(

@@ -30,6 +30,13 @@ constexpr int kBlock = PERT_BLOCK;
 constexpr int kWaves = kBlock / 64;
 constexpr int kDefaultLT = 32;
 constexpr int kMaxLT = 64;
+#ifndef PERT_ENUM3_ORDER
+#define PERT_ENUM3_ORDER 0
+#endif
+// variant 3's workgroup -> (cell tile, bin tile) order (the dispatcher deals consecutive
+// workgroup ids round robin over the 8 XCDs): 0 cell tiles fastest, 1 bin tiles fastest,
+// 2 / 3 XCD-aware -- XCD k runs a contiguous eighth of the tiles in bin- / cell-fastest order
+constexpr int kEnum3Order = PERT_ENUM3_ORDER;
 constexpr int kShortLT3 = 12;                    // variant 3's tile length on multi-round launches
 constexpr int kLongLT3 = 18;                     // ... and on launches of 8 rounds or more
 constexpr int kEtaLdsFloats = 1024;   // eta tables up to 4 KB are staged in LDS
@@ -558,6 +565,27 @@ __device__ __forceinline__ void store_nt(__amdgpu_buffer_rsrc_t rs, float v, uin
                                         PERT_NT_STORE ? PERT_STORE_CPOL : 0);
 }
 
+// (cell tile, bin tile) of this workgroup of a variant-3 launch (grid from enum3_grid)
+__device__ __forceinline__ bool enum3_tile(int n_ct, int n_bt, int& wt, int& bt) {
+  if constexpr (kEnum3Order == 0) {
+    wt = blockIdx.x;
+    bt = blockIdx.y;
+    return true;
+  } else if constexpr (kEnum3Order == 1) {
+    wt = blockIdx.y;
+    bt = blockIdx.x;
+    return true;
+  } else {
+    const int T = n_ct * n_bt, per = (T + 7) / 8;
+    const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+    if (w >= T) return false;
+    constexpr bool bin_fast = kEnum3Order == 2;
+    wt = bin_fast ? w / n_bt : w % n_ct;
+    bt = bin_fast ? w % n_bt : w / n_ct;
+    return true;
+  }
+}
+
 template <int K1T>
 __device__ void enum3_fused_tail(const pert_problem& pr, const pert_state& st, const pert_adam_hparams& hp, int wt,
                                  int by, int lane, bool update_shared);
@@ -585,11 +613,12 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
   const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
 #endif
   const int N = pr.N, K1 = (K1T == PERT_MAX_K1) ? pr.K1 : K1T, ldn = pr.ldn;
-  const int wt = blockIdx.x;
+  const int LT = st.bins_per_tile;
+  int wt, bt;
+  if (!enum3_tile((N + 63) / 64, (pr.L + LT - 1) / LT, wt, bt)) return;   // (the grid's round-up)
   const int n = wt * 64 + lane;
   const bool valid = n < N;
-  const int LT = st.bins_per_tile;
-  const int l0 = blockIdx.y * LT;
+  const int l0 = bt * LT;
   const int l1 = min(pr.L, l0 + LT);
   const int nb = l1 - l0;
   const bool frozen = pr.kind == PERT_KIND_STEP3;
@@ -813,7 +842,7 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
   }
   if (kDecode) return;
   if (valid) {
-    float* cp = st.cell_part + (size_t)blockIdx.y * (K1 + 1) * N + n;
+    float* cp = st.cell_part + (size_t)bt * (K1 + 1) * N + n;
 #pragma unroll
     for (int k = 0; k < K1T; ++k) {
       if (k >= K1) continue;
@@ -826,7 +855,7 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
   const double bl = wave_sum_d((double)loss);
   const double bga = wave_sum_d((double)ga);
   if (lane == 0) {
-    double* bp = st.blk_part + ((size_t)blockIdx.y * (ldn / 64) + wt) * kBlkSlots;
+    double* bp = st.blk_part + ((size_t)bt * (ldn / 64) + wt) * kBlkSlots;
     if (coh) {
       st_coh(bp, bl);
       st_coh(bp + 1, bga);
@@ -835,7 +864,7 @@ __global__ void __launch_bounds__(64, PERT_ENUM3_WAVES) enum3_kernel(pert_proble
       bp[1] = bga;
     }
   }
-  if (kStep && fuse) enum3_fused_tail<K1T>(pr, st, hp, wt, blockIdx.y, lane, fuse == 2);
+  if (kStep && fuse) enum3_fused_tail<K1T>(pr, st, hp, wt, bt, lane, fuse == 2);
 #ifdef PERT_ENUM3_STAMPS
   if (kStep && lane == 0) {
     dbg[0] = t_entry;
@@ -1988,9 +2017,11 @@ __global__ void __launch_bounds__(kBlock) adam_kernel(pert_problem pr, pert_stat
 // its time is what this access pattern costs in HBM on the box it runs on.
 template <int P>
 __global__ void __launch_bounds__(64) stream_ceiling_kernel(pert_problem pr, pert_state st) {
-  const int lane = threadIdx.x, wt = blockIdx.x, ldn = pr.ldn;
+  const int lane = threadIdx.x, ldn = pr.ldn;
   const int LT = st.bins_per_tile;
-  const int l0 = blockIdx.y * LT, l1 = min(pr.L, l0 + LT);
+  int wt, bt;                                                   // the three-wave pass's tile order
+  if (!enum3_tile((pr.N + 63) / 64, (pr.L + LT - 1) / LT, wt, bt)) return;
+  const int l0 = bt * LT, l1 = min(pr.L, l0 + LT);
   const size_t t0 = (size_t)wt * pr.L * P * 64 + lane;
   float zr[P], mr[P], vr[P];
   float xr = 0.0f;
@@ -2082,6 +2113,14 @@ size_t dma_lds_bytes(int P, int mode, const pert_state& st, const pert_problem& 
 int enum_cell_tiles(const pert_problem* pr, const pert_state* st) {
   (void)st;
   return (pr->N + 63) / 64;
+}
+
+// the grid of a variant-3 launch (and of its pattern-ceiling kernel) in kEnum3Order
+dim3 enum3_grid(const pert_problem* pr, const pert_state* st, int lt) {
+  const unsigned n_ct = (unsigned)enum_cell_tiles(pr, st), n_bt = (unsigned)((pr->L + lt - 1) / lt);
+  if (kEnum3Order == 0) return dim3(n_ct, n_bt);
+  if (kEnum3Order == 1) return dim3(n_bt, n_ct);
+  return dim3((n_ct * n_bt + 7) / 8 * 8);
 }
 
 // the enumerated-pass variants this library carries: 0 (LDS-DMA, two waves per SIMD),
@@ -2342,7 +2381,8 @@ int pert_enum_pass(const pert_problem* prob, pert_state* st, const pert_adam_hpa
     return PERT_E_ARG;
   pert_state s2 = *st;
   s2.bins_per_tile = tile_bins(st);
-  const dim3 grid(enum_cell_tiles(prob, st), (prob->L + s2.bins_per_tile - 1) / s2.bins_per_tile);
+  const dim3 grid = st->variant == 3 ? enum3_grid(prob, st, s2.bins_per_tile)
+                                     : dim3(enum_cell_tiles(prob, st), (prob->L + s2.bins_per_tile - 1) / s2.bins_per_tile);
   switch (mode) {
     case PERT_MODE_STEP: return launch_enum_mode<PERT_MODE_STEP>(prob->P, grid, *prob, s2, *hp, stream);
     case PERT_MODE_GRAD: return launch_enum_mode<PERT_MODE_GRAD>(prob->P, grid, *prob, s2, *hp, stream);
@@ -2364,7 +2404,7 @@ int pert_enum_step(const pert_problem* prob, pert_state* st, const pert_adam_hpa
     return PERT_E_ARG;
   pert_state s2 = *st;
   s2.bins_per_tile = tile_bins(st);
-  const dim3 grid(enum_cell_tiles(prob, st), (prob->L + s2.bins_per_tile - 1) / s2.bins_per_tile);
+  const dim3 grid = enum3_grid(prob, st, s2.bins_per_tile);
   return launch_enum_mode<PERT_MODE_STEP>(prob->P, grid, *prob, s2, *hp, stream, update_shared ? 2 : 1);
 }
 
@@ -2551,7 +2591,7 @@ int pert_stream_ceiling(const pert_problem* prob, pert_state* st, hipStream_t st
   if (prob->kind != PERT_KIND_STEP2 && prob->kind != PERT_KIND_STEP3) return PERT_E_ARG;
   pert_state s2 = *st;
   s2.bins_per_tile = tile_bins(st);
-  const dim3 grid(enum_cell_tiles(prob, st), (prob->L + s2.bins_per_tile - 1) / s2.bins_per_tile);
+  const dim3 grid = enum3_grid(prob, st, s2.bins_per_tile);
   switch (prob->P) {
 #define PERT_CASE(PP)                                                                          \
   case PP:                                                                                     \

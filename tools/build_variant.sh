@@ -8,7 +8,8 @@ T=$(mktemp -d)
 HIPCC="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-slp-vectorize -fno-signed-zeros"
 $HIPCC "$@" -I $R/include -c $R/scdna_replication_tools_amd/csrc/pert_kernels.hip -o $T/k.o
 $HIPCC -I $R/include -c $R/scdna_replication_tools_amd/csrc/tau_kernels.hip -o $T/tau.o
+$HIPCC -I $R/include -c $R/scdna_replication_tools_amd/csrc/pert_comm.hip -o $T/comm.o
 echo "const char* pert_version(void) { return \"pert_hip variant gfx950 flags=$*\"; }" > $T/v.c
 gcc -O2 -fPIC -c $T/v.c -o $T/v.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $T/k.o $T/tau.o $T/v.o -o $OUT
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $T/k.o $T/tau.o $T/comm.o $T/v.o -o $OUT
 rm -rf $T

@@ -12,7 +12,8 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++20 tools/depth_probe.hip -o tools/depth_probe
 //   ./depth_probe [cells=1250] [bins=5451] [LT=54] [waves_per_cu=12] [iters=20] [spread=1] [swap=0]
 // spread: cell tiles placed spread x a tile apart (the footprint of a spread x larger shard);
-// swap: blockIdx.x walks the bin tiles instead of the cell tiles.
+// swap: the workgroup -> tile order: 0 cell tiles fastest (the pass's), 1 bin tiles fastest,
+// 2 / 3 XCD-aware (XCD k gets a contiguous eighth of the tiles, bin- / cell-fastest).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -32,11 +33,23 @@ constexpr int P = 13;
 template <int D>
 __global__ void __launch_bounds__(64) depth_stream(const float* __restrict__ x, const uint16_t* __restrict__ code,
                                                    float* z, float* m, float* v, int L, int ldn, int LT, int spread,
-                                                   int swap, float* sink) {
+                                                   int swap, int n_ct, float* sink) {
   extern __shared__ float pad[];                  // occupancy cap: dynamic LDS per workgroup
   const int lane = threadIdx.x;
   if (lane == 0 && LT < 0) pad[0] = 0.0f;
-  const int wt = swap ? blockIdx.y : blockIdx.x, bt = swap ? blockIdx.x : blockIdx.y;
+  // tile of this workgroup (1-D grid of n_ct x n_bt; the dispatcher deals consecutive ids round
+  // robin over the 8 XCDs): 0 cell tiles fastest, 1 bin tiles fastest, 2 / 3 XCD-aware -- XCD k
+  // runs a contiguous 1/8 of the tiles in bin-fastest (2) / cell-fastest (3) order
+  const int n_bt = (L + LT - 1) / LT, T = n_ct * n_bt;
+  int w = blockIdx.x;
+  if (swap >= 2) {
+    const int per = (T + 7) / 8, xcd = w % 8, slot = w / 8;
+    w = xcd * per + slot;
+    if (w >= T) return;
+  }
+  const bool bin_fast = swap == 1 || swap == 2;
+  const int wt = bin_fast ? w / n_bt : w % n_ct, bt = bin_fast ? w % n_bt : w / n_ct;
+
   const int l0 = bt * LT, l1 = min(L, l0 + LT);
   const size_t t0 = ((size_t)wt * spread * L) * P * 64 + lane;     // spread: tiles apart by spread x a tile
   float zr[D][P], mr[D][P], vr[D][P], xr[D];
@@ -132,7 +145,8 @@ int main(int argc, char** argv) {
   CK(hipMemset(code, 0, (size_t)L * ldn * 2));
   const double bytes = (double)nwt * 64 * L * (6.0 + 24.0 * P);   // the launched tiles' bytes
   const int nbt = (L + LT - 1) / LT;
-  const dim3 grid(swap ? nbt : nwt, swap ? nwt : nbt);
+  const int T = nwt * nbt;
+  const dim3 grid(swap >= 2 ? (T + 7) / 8 * 8 : T);
   const size_t lds = (size_t)(160 * 1024) / wpc - 256;
   int dev = 0, ncu = 0;
   CK(hipGetDevice(&dev));
@@ -141,9 +155,9 @@ int main(int argc, char** argv) {
   CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[0], depth_stream<1>, 64, lds));
   CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1], depth_stream<2>, 64, lds));
   CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[2], depth_stream<3>, 64, lds));
-  const float t1 = time_ms([&] { depth_stream<1><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, sink); }, iters);
-  const float t2 = time_ms([&] { depth_stream<2><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, sink); }, iters);
-  const float t3 = time_ms([&] { depth_stream<3><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, sink); }, iters);
+  const float t1 = time_ms([&] { depth_stream<1><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, nwt, sink); }, iters);
+  const float t2 = time_ms([&] { depth_stream<2><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, nwt, sink); }, iters);
+  const float t3 = time_ms([&] { depth_stream<3><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, nwt, sink); }, iters);
   printf("spread %d swap %d cells %d bins %d LT %d tiles %d (%.2f rounds of %d x %d slots): depth1 %.4f ms %.3f TB/s | depth2 %.4f ms "
          "%.3f TB/s | depth3 %.4f ms %.3f TB/s (occupancy %d/%d/%d)\n",
          spread, swap, N, L, LT, nwt * nbt, (double)nwt * nbt / ((double)ncu * occ[0]), ncu, occ[0], t1, bytes / t1 / 1e9, t2,

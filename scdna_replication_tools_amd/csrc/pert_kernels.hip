@@ -31,11 +31,15 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kDefaultLT = 32;
 constexpr int kMaxLT = 64;
 #ifndef PERT_ENUM3_ORDER
-#define PERT_ENUM3_ORDER 0
+#define PERT_ENUM3_ORDER 2
 #endif
 // variant 3's workgroup -> (cell tile, bin tile) order (the dispatcher deals consecutive
 // workgroup ids round robin over the 8 XCDs): 0 cell tiles fastest, 1 bin tiles fastest,
-// 2 / 3 XCD-aware -- XCD k runs a contiguous eighth of the tiles in bin- / cell-fastest order
+// 2 / 3 XCD-aware -- XCD k runs a contiguous eighth of the tiles in bin- / cell-fastest order.
+// 2 (default): each XCD streams its own contiguous run of the tile-major z / m / v arrays, bins
+// of a cell tile in order; interleaved A/B on one box (profiles/r05f_tile_order_ab.log): C4
+// pass 3.444-3.455 vs 3.478-3.481 ms and its pattern ceiling 3.34 vs 3.43 ms, the 1,250-cell
+// shard's pass 0.464-0.467 vs 0.468-0.471 ms (order 1 alone: +5 % there, order 3: no gain)
 constexpr int kEnum3Order = PERT_ENUM3_ORDER;
 constexpr int kShortLT3 = 12;                    // variant 3's tile length on multi-round launches
 constexpr int kLongLT3 = 18;                     // ... and on launches of 8 rounds or more

@@ -404,6 +404,14 @@ def main():
         shard.run_svi(args.warmup, min_iter=10 ** 9, rel_tol=0.0)
     # the loop's buffers (and step 1's canonical pi trajectory) set up before the timed region,
     # as run_pert_model has them ready before a fit starts
+    # Before the timed region, the pattern's HBM ceiling on this device and lease (pert_stream_ceiling:
+    # the pass's streams with no arithmetic, the state left unchanged), repeated for ~100 ms of
+    # HBM load: on a short shard the first timed steps otherwise run ~3 % slower than the next
+    # ones (r05g: 1,250 cells 0.510 ms/step in the first K steps after W = 3, 0.495 in the next K)
+    ceil_ms = None
+    if args.fit != "step1":
+        est = shard.stream_ceiling_ms(reps=3)
+        ceil_ms = shard.stream_ceiling_ms(reps=int(min(200, max(10, math.ceil(100.0 / max(est, 1e-3))))))
     # The value's region is the production loop with no timing events (one C call, pert_svi_run):
     # a HIP timing event on the stream costs the step ~50 us (r05d: 0.497 vs 0.520 ms/step at
     # 1,250 cells with events around every 5th pass).  The pass durations come from the same K
@@ -436,9 +444,6 @@ def main():
     dt_ev = time.perf_counter() - t1
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in shard.pass_events]))
     shard.pass_events = None
-    # after the timed region: the same shard's HBM streams with no arithmetic (the pattern's
-    # ceiling on this device, this lease) -- pert_stream_ceiling leaves the state unchanged
-    ceil_ms = shard.stream_ceiling_ms() if args.fit != "step1" else None
     t = torch.tensor([dt, kern_ms, dt_ev], dtype=torch.float64, device=device)
     if pg is not None:
         pg.all_reduce(t, op=pg.ReduceOp.MAX)

@@ -14,32 +14,32 @@ import sys
 
 def main(path):
     rows = [json.loads(l) for l in open(path) if l.strip().startswith("{")]
-    reps = {}
+    # (r05d lines: ms_per_step evented, ms_per_step_no_events plain; later: ms_per_step plain,
+    # ms_per_step_evented)
+    ev = lambda r: r.get("ms_per_step_evented", r["ms_per_step"])
+    plain = lambda r: r["ms_per_step"] if "ms_per_step_evented" in r else r.get("ms_per_step_no_events",
+                                                                                r["ms_per_step"])
+    groups = {}
     for r in rows:
-        key = (r.get("_rep"), r["config"]["cells"], bool(r.get("_fused")))
-        reps[key] = r
-    for rep in sorted({k[0] for k in reps}):
-        base = reps.get((rep, 10000, False))
+        groups.setdefault((r["config"]["bins"], r.get("_rep")), {})[(r["config"]["cells"], bool(r.get("_fused")))] = r
+    for (bins, rep), g in sorted(groups.items()):
+        big = max(c for c, f in g)
+        base = g.get((big, False))
         if base is None:
             continue
-        # (r05d lines: ms_per_step evented, ms_per_step_no_events plain; later: ms_per_step plain,
-        # ms_per_step_evented)
-        ev = lambda r: r.get("ms_per_step_evented", r["ms_per_step"])
-        plain = lambda r: r["ms_per_step"] if "ms_per_step_evented" in r else r.get("ms_per_step_no_events",
-                                                                                    r["ms_per_step"])
         t_ev, t_plain = ev(base), plain(base)
-        print("rep {}: 10,000 cells {:.4f} ms/step (no events {:.4f}), pass {:.4f} ms, ceiling {:.4f} ms".format(
-            rep, t_ev, t_plain, base["roofline"]["kernel_ms"], base["roofline"]["pattern_ceiling"]["ms"]))
-        for (rp, cells, fused), r in sorted(reps.items()):
-            if rp != rep or cells == 10000:
+        print("rep {}: {:,} cells x {:,} bins {:.4f} ms/step (evented run {:.4f}), pass {:.4f} ms, ceiling {:.4f} ms".format(
+            rep, big, bins, t_plain, t_ev, base["roofline"]["kernel_ms"], base["roofline"]["pattern_ceiling"]["ms"]))
+        for (cells, fused), r in sorted(g.items()):
+            if cells == big:
                 continue
-            n = round(10000 / cells)
+            n = round(big / cells)
             s_ev, s_plain = ev(r), plain(r)
             k, c = r["roofline"]["kernel_ms"], r["roofline"]["pattern_ceiling"]["ms"]
-            print("  N={} shard {:5d} cells{}: {:.4f} ms/step (no events {:.4f}), pass {:.4f} ms = {:.3f} of its "
-                  "ceiling {:.4f}; efficiency {:.1%} (no events {:.1%}); allreduce: {}".format(
-                      n, cells, " fused" if fused else "", s_ev, s_plain, k, c / k, c, t_ev / (n * s_ev),
-                      t_plain / (n * s_plain), r["config"]["allreduce"][:40]))
+            print("  N={} shard {:5d} cells{}: {:.4f} ms/step (evented run {:.4f}), pass {:.4f} ms = {:.3f} of its "
+                  "ceiling {:.4f}; efficiency {:.1%} (evented runs {:.1%}); allreduce: {}".format(
+                      n, cells, " fused" if fused else "", s_plain, s_ev, k, c / k, c, t_plain / (n * s_plain),
+                      t_ev / (n * s_ev), r["config"]["allreduce"][:40]))
 
 
 if __name__ == "__main__":

@@ -365,12 +365,20 @@ def main():
         t_init = np.clip(data["tau"][n0:n1].cpu().numpy(), 0.05, 0.95)
         prior_desc = "g1_clones (weight 1e6)"
     ploidy = eta.argmax_states().mean(0)
-    comm = None
+    comm, comm_error = None, None
     if args.comm == "rccl" or (args.comm == "auto" and world > 1 and backend == "nccl"):
-        comm = RcclComm() if world > 1 else RcclComm.world1()
+        try:
+            comm = RcclComm() if world > 1 else RcclComm.world1()
+        except Exception as e:                     # noqa: BLE001  (then torch.distributed's all-reduce)
+            if args.comm == "rccl":
+                raise
+            comm_error = "{}: {}".format(type(e).__name__, e)
+            print("bench: the library's RCCL communicator failed ({}); all-reducing through "
+                  "torch.distributed".format(comm_error), file=sys.stderr, flush=True)
     allreduce = comm.allreduce if comm is not None else make_allreduce()
     comm_desc = ("rccl: the library's own communicator, all-reduce queued inside the C loop (pert_svi_run_sharded)"
-                 if comm is not None else "torch.distributed all_reduce per step from Python" if allreduce is not None
+                 if comm is not None else "torch.distributed all_reduce per step from Python{}".format(
+                     " (pert_comm failed: {})".format(comm_error) if comm_error else "") if allreduce is not None
                  else "none (one rank)")
     libs = np.zeros(n1 - n0, int)
     common = dict(device=device, is_root=(rank == 0), allreduce=allreduce, bins_per_tile=args.bins_per_tile,

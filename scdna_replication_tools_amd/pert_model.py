@@ -125,7 +125,11 @@ class _Dist:
         self.comm = None
         if self.world > 1 and self.backend == "nccl" and os.environ.get("PERT_NATIVE_COMM", "1") != "0":
             from .engine import RcclComm
-            self.comm = RcclComm(group)
+            try:
+                self.comm = RcclComm(group)
+            except Exception as e:                 # noqa: BLE001  (torch.distributed's all-reduce then)
+                log.warning("the library's RCCL communicator failed (%s: %s); all-reducing through "
+                            "torch.distributed per step", type(e).__name__, e)
         self.allreduce = (self.comm.allreduce if self.comm is not None else
                           make_allreduce(group) if self.world > 1 else None)
 

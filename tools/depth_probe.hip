@@ -12,6 +12,8 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++20 tools/depth_probe.hip -o tools/depth_probe
 //   ./depth_probe [cells=1250] [bins=5451] [LT=54] [waves_per_cu=12] [iters=20] [spread=1] [swap=0]
 // spread: cell tiles placed spread x a tile apart (the footprint of a spread x larger shard);
+// work (8th argument, > 0): the load-schedule experiment instead -- that many VALU operations per
+// bin between the loads and the stores, m / v loaded in the bin that uses them or a bin ahead.
 // swap: the workgroup -> tile order: 0 cell tiles fastest (the pass's), 1 bin tiles fastest,
 // 2 / 3 XCD-aware (XCD k gets a contiguous eighth of the tiles, bin- / cell-fastest).
 #include <hip/hip_runtime.h>
@@ -102,6 +104,79 @@ __global__ void __launch_bounds__(64) depth_stream(const float* __restrict__ x, 
   if (acc == 12345.678f) sink[0] = acc;
 }
 
+// The pass's load schedule with arithmetic in between: per bin, `work` VALU operations (four
+// independent fma chains on the bin's z values) between the issue of the next loads and the
+// stores.  mv_ahead 0: as enum3_kernel -- x, code, z of bin l+1 and m, v of bin l issued at the top
+// of bin l, m and v consumed after the arithmetic; 1: m, v of bin l+1 issued a bin ahead as well.
+template <int MV_AHEAD>
+__global__ void __launch_bounds__(64) work_stream(const float* __restrict__ x, const uint16_t* __restrict__ code,
+                                                  float* z, float* m, float* v, int L, int ldn, int LT, int n_ct,
+                                                  int work, float* sink) {
+  extern __shared__ float pad[];
+  const int lane = threadIdx.x;
+  if (lane == 0 && LT < 0) pad[0] = 0.0f;
+  const int n_bt = (L + LT - 1) / LT, T = n_ct * n_bt, per = (T + 7) / 8;
+  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  if (w >= T) return;
+  const int wt = w / n_bt, bt = w % n_bt;
+  const int l0 = bt * LT, l1 = min(L, l0 + LT);
+  const size_t t0 = ((size_t)wt * L) * P * 64 + lane;
+  float zr[P], mr[P], vr[P], xr = 0.0f;
+  uint32_t cr = 0;
+  auto load_zxc = [&](int l) {
+    const size_t o = t0 + (size_t)l * P * 64;
+#pragma unroll
+    for (int k = 0; k < P; ++k) zr[k] = __builtin_nontemporal_load(z + o + k * 64);
+    xr = x[(size_t)l * ldn + wt * 64 + lane];
+    cr = code[(size_t)l * ldn + wt * 64 + lane];
+  };
+  auto load_mv = [&](int l) {
+    const size_t o = t0 + (size_t)l * P * 64;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      mr[k] = __builtin_nontemporal_load(m + o + k * 64);
+      vr[k] = __builtin_nontemporal_load(v + o + k * 64);
+    }
+  };
+  float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f, acc3 = 0.0f;
+  load_zxc(l0);
+  if (MV_AHEAD) load_mv(l0);
+  for (int l = l0; l < l1; ++l) {
+    float zc[P], mc[P], vc[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) zc[k] = zr[k];
+    float xc = xr + (float)cr;
+    if (MV_AHEAD) {
+#pragma unroll
+      for (int k = 0; k < P; ++k) { mc[k] = mr[k]; vc[k] = vr[k]; }
+    }
+    if (l + 1 < l1) {
+      load_zxc(l + 1);
+      if (MV_AHEAD) load_mv(l + 1);
+    }
+    if (!MV_AHEAD) load_mv(l);
+    for (int i = 0; i < work; i += 4) {
+      acc0 = __builtin_fmaf(acc0, 0.999f, zc[(i >> 2) % P]);
+      acc1 = __builtin_fmaf(acc1, 0.998f, xc);
+      acc2 = __builtin_fmaf(acc2, 0.997f, zc[((i >> 2) + 5) % P]);
+      acc3 = __builtin_fmaf(acc3, 0.996f, xc * 0.5f);
+    }
+    if (!MV_AHEAD) {
+#pragma unroll
+      for (int k = 0; k < P; ++k) { mc[k] = mr[k]; vc[k] = vr[k]; }
+    }
+    const size_t o = t0 + (size_t)l * P * 64;
+    const float g = (acc0 + acc1) * 1e-30f + (acc2 + acc3) * 1e-30f;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      __builtin_nontemporal_store(zc[k] + g, z + o + k * 64);
+      __builtin_nontemporal_store(mc[k] + g, m + o + k * 64);
+      __builtin_nontemporal_store(vc[k] + g, v + o + k * 64);
+    }
+  }
+  if (acc0 + acc1 + acc2 + acc3 == 12345.678f) sink[0] = acc0;
+}
+
 template <class F>
 static float time_ms(F f, int iters) {
   hipEvent_t e0, e1;
@@ -158,6 +233,18 @@ int main(int argc, char** argv) {
   const float t1 = time_ms([&] { depth_stream<1><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, nwt, sink); }, iters);
   const float t2 = time_ms([&] { depth_stream<2><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, nwt, sink); }, iters);
   const float t3 = time_ms([&] { depth_stream<3><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, nwt, sink); }, iters);
+  const int work = argc > 8 ? atoi(argv[8]) : 0;
+  if (work > 0) {                         // the schedule experiment (work_stream), order 2
+    const dim3 g1((nwt * nbt + 7) / 8 * 8);
+    const float a0 = time_ms([&] { work_stream<0><<<g1, 64, lds>>>(x, code, z, m, v, L, ldn, LT, nwt, work, sink); }, iters);
+    const float a1 = time_ms([&] { work_stream<1><<<g1, 64, lds>>>(x, code, z, m, v, L, ldn, LT, nwt, work, sink); }, iters);
+    int o0 = 0, o1 = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o0, work_stream<0>, 64, lds));
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, work_stream<1>, 64, lds));
+    printf("work %d cells %d LT %d: m/v same bin %.4f ms %.3f TB/s | m/v a bin ahead %.4f ms %.3f TB/s (occupancy %d/%d)\n",
+           work, N, LT, a0, bytes / a0 / 1e9, a1, bytes / a1 / 1e9, o0, o1);
+    return 0;
+  }
   printf("spread %d swap %d cells %d bins %d LT %d tiles %d (%.2f rounds of %d x %d slots): depth1 %.4f ms %.3f TB/s | depth2 %.4f ms "
          "%.3f TB/s | depth3 %.4f ms %.3f TB/s (occupancy %d/%d/%d)\n",
          spread, swap, N, L, LT, nwt * nbt, (double)nwt * nbt / ((double)ncu * occ[0]), ncu, occ[0], t1, bytes / t1 / 1e9, t2,

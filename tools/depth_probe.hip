@@ -155,11 +155,15 @@ __global__ void __launch_bounds__(64) work_stream(const float* __restrict__ x, c
       if (MV_AHEAD) load_mv(l + 1);
     }
     if (!MV_AHEAD) load_mv(l);
-    for (int i = 0; i < work; i += 4) {
-      acc0 = __builtin_fmaf(acc0, 0.999f, zc[(i >> 2) % P]);
-      acc1 = __builtin_fmaf(acc1, 0.998f, xc);
-      acc2 = __builtin_fmaf(acc2, 0.997f, zc[((i >> 2) + 5) % P]);
-      acc3 = __builtin_fmaf(acc3, 0.996f, xc * 0.5f);
+    for (int i = 0; i < work; i += 8) {                  // (constant register indices only)
+      acc0 = __builtin_fmaf(acc0, 0.999f, zc[0]);
+      acc1 = __builtin_fmaf(acc1, 0.998f, zc[1]);
+      acc2 = __builtin_fmaf(acc2, 0.997f, zc[2]);
+      acc3 = __builtin_fmaf(acc3, 0.996f, xc);
+      acc0 = __builtin_fmaf(acc0, 0.995f, zc[3]);
+      acc1 = __builtin_fmaf(acc1, 0.994f, zc[4]);
+      acc2 = __builtin_fmaf(acc2, 0.993f, zc[5]);
+      acc3 = __builtin_fmaf(acc3, 0.992f, zc[6]);
     }
     if (!MV_AHEAD) {
 #pragma unroll

@@ -337,3 +337,50 @@ def test_row_state_counts_equals_bincount():
         want = np.stack([np.bincount(r, minlength=V) for r in st])
         np.testing.assert_array_equal(prep._row_state_counts(st, V), want)
         np.testing.assert_array_equal(prep._row_state_counts(st.astype(np.float64), V), want)
+
+
+@pytest.mark.parametrize("kind", [1, 2, 3])
+@pytest.mark.parametrize("method", ["sampled", "median"])
+def test_init_params_of_a_cell_range_equal_the_whole_fits(kind, method):
+    """init_params(cells=...) -- one rank's shard of a sharded fit -- gives exactly the whole
+    fit's initial values of those cells (the generator still draws for every cell), with
+    t_init / ploidy given for the rank's cells only; the shared sites are the whole fit's."""
+    from scdna_replication_tools_amd.init import init_params
+    rng = np.random.default_rng(3)
+    L, N, n_libs = 40, 37, 2
+    reads = rng.poisson(100, (L, N)).astype(np.float32)
+    libs = rng.integers(0, n_libs, N)
+    ploidy = rng.uniform(1.5, 3.0, N)
+    t_init = rng.uniform(0.05, 0.95, N)
+    bm = rng.normal(size=(n_libs, 5))
+    kw = dict(beta_means=bm, seed=7, method=method)
+    whole = init_params(kind, reads, libs, n_libs, 13, 4, ploidy=ploidy, t_init=t_init, **kw)
+    for sl in (slice(0, 19), slice(19, N), slice(5, 6)):
+        part = init_params(kind, reads, libs, n_libs, 13, 4, ploidy=ploidy[sl], t_init=t_init[sl], cells=sl, **kw)
+        assert set(part) == set(whole)
+        for k, v in whole.items():
+            want = v[sl] if k in ("expose_tau", "expose_u", "expose_betas") else v
+            np.testing.assert_array_equal(part[k], want, err_msg=k)
+
+
+def test_clone_prior_of_a_cell_range_equals_the_whole_prior_sliced():
+    """build_clone_cn_prior(cell_range=...) -- one rank's code book -- equals the whole code
+    book's columns of those cells; an out-of-range clone state raises on every rank alike."""
+    from scdna_replication_tools_amd.simulator import simulate, to_long_form
+    from scdna_replication_tools_amd.pert_model import pert_infer_scRT
+    sim = simulate(n_s=23, n_g=30, n_bins=300, num_reads=300 * 183, seed=8, n_clones=3)
+    s, g = to_long_form(sim, n_libs=1)
+    m = pert_infer_scRT(s, g, input_col='reads', clone_col='clone_id', cn_prior_method='g1_clones', device="cpu")
+    inp = m._prepare()
+    profiles = prep.consensus_clone_profiles(m.cn_g1, m.cn_state_col, keys=inp.keys_g)
+    whole = m._build_etas(inp, profiles)
+    for sl in (slice(0, 12), slice(12, 23)):
+        part = m._build_etas(inp, profiles, cells=sl)
+        np.testing.assert_array_equal(part.codes, whole.codes[:, sl])
+        np.testing.assert_array_equal(part.table, whole.table)
+        np.testing.assert_array_equal(part.ploidy(), whole.ploidy()[sl])
+    for method in ("hmmcopy", "diploid", "uniform", "g1_composite"):
+        m.cn_prior_method = method
+        w = m._build_etas(inp, profiles)
+        p = m._build_etas(inp, profiles, cells=slice(3, 17))
+        np.testing.assert_array_equal(p.dense(), w.dense()[:, 3:17], err_msg=method)

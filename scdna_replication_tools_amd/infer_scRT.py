@@ -25,8 +25,14 @@ def assign_s_to_clones(s_phase_cells: pd.DataFrame, clone_df: pd.DataFrame, col_
     # per-cell blocks (the concatenated per-cell tables of the tutorials): the pivot is a
     # transpose of the blocks and every row's cell is its block's -- no per-row hashing
     lay = prep._block_layout(s_phase_cells, cell_col, chr_col, start_col, col_name)
-    s = s_phase_cells.copy()
-    s[chr_col] = s[chr_col].astype(str)
+    # a new frame over the same column blocks (the reference mutates and returns its argument;
+    # the new columns below are set on this frame only)
+    s = s_phase_cells.copy(deep=False)
+    chc = s[chr_col]
+    if lay is not None and chc.dtype == object and all(isinstance(v, str) for v in chc.to_numpy()[:lay[1]]):
+        pass             # every block holds block 0's label objects (_block_layout): already str
+    else:
+        s[chr_col] = chc.astype(str)
     clone_df = clone_df.copy()
     if set([chr_col, start_col]).issubset(set(clone_df.columns)):
         clone_df = clone_df.set_index([chr_col, start_col])
@@ -63,7 +69,10 @@ def assign_s_to_clones(s_phase_cells: pd.DataFrame, clone_df: pd.DataFrame, col_
         # -1 in the pandas the reference ran on, i.e. the last clone
         best.append(clone_df.columns[int(np.nanargmax(r)) if np.isfinite(r).any() else -1])
     if row_cell is not None:
-        s[clone_col] = pd.Series(np.asarray(best, dtype=object)[row_cell], index=s.index).infer_objects()
+        # the per-cell labels' dtype as infer_objects finds it for the rows (the same set of
+        # values), then one gather per row
+        per_cell = pd.Series(np.asarray(best, dtype=object)).infer_objects().to_numpy()
+        s[clone_col] = pd.Series(per_cell[row_cell], index=s.index)
     else:
         lut = dict(zip(piv.cells, best))
         s[clone_col] = s[cell_col].astype(str).map(lut)
@@ -174,10 +183,24 @@ class scRT:
             clusters = kmeans_cluster(g1_mat, max_k=20, device=self.engine_kwargs.get("device"))
             self.clusters = clusters
             # pd.merge(cn_g1, clusters, on=cell_col) for an inner join on a complete cluster table
-            lut = pd.Series(clusters["cluster_id"].to_numpy(), index=clusters["cell_id"].to_numpy())
-            self.cn_g1 = self.cn_g1.assign(cluster_id=self.cn_g1[self.cell_col].map(lut))
-            self.cn_g1 = self.cn_g1[self.cn_g1["cluster_id"].notna()]
-            self.cn_g1["cluster_id"] = self.cn_g1["cluster_id"].astype(np.int64)
+            cid = clusters["cluster_id"].to_numpy().astype(np.int64)
+            lay = prep._block_layout(self.cn_g1, self.cell_col, self.chr_col, self.start_col, None)
+            row_cl = None
+            if lay is not None:
+                # per-cell blocks: a row's cell is its block's (no per-row label lookup)
+                B, L = lay[0], lay[1]
+                heads = np.ascontiguousarray(self.cn_g1[self.cell_col].to_numpy())[::L]
+                ci = pd.Index(clusters["cell_id"].to_numpy()).get_indexer(heads)
+                if (ci >= 0).all():
+                    row_cl = np.repeat(cid[ci], L)
+            if row_cl is not None:
+                self.cn_g1 = self.cn_g1.copy(deep=False)
+                self.cn_g1["cluster_id"] = row_cl
+            else:
+                lut = pd.Series(cid, index=clusters["cell_id"].to_numpy())
+                self.cn_g1 = self.cn_g1.assign(cluster_id=self.cn_g1[self.cell_col].map(lut))
+                self.cn_g1 = self.cn_g1[self.cn_g1["cluster_id"].notna()]
+                self.cn_g1["cluster_id"] = self.cn_g1["cluster_id"].astype(np.int64)
             self.clone_col = 'cluster_id'
         self.clone_profiles = consensus_profiles(
             self.cn_g1, self.assign_col, clone_col=self.clone_col, cell_col=self.cell_col, chr_col=self.chr_col,

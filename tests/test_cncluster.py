@@ -71,3 +71,31 @@ def test_kmeans_fit_inertia_matches_sklearn():
     _, _, inertia = kmeans_fit(X, 4, n_init=10, device="cpu")
     ref = sklearn.cluster.KMeans(n_clusters=4, init="k-means++", n_init=10, random_state=0).fit(X).inertia_
     assert np.isclose(inertia, ref, rtol=1e-9)
+
+
+def test_clustered_labels_block_path_equals_general_path(monkeypatch):
+    """scRT(clone_col=None): the G1/2 table's cluster_id column and the S cells' assigned
+    clones from the per-cell-block fast paths equal the general paths' (label lookups per row,
+    the reference's merge and per-cell assignment), dtypes included."""
+    from scdna_replication_tools_amd import infer_scRT as isc
+    from scdna_replication_tools_amd import prep
+    from scdna_replication_tools_amd.simulator import simulate, to_long_form
+    sim = simulate(n_s=24, n_g=45, n_bins=300, num_reads=300 * 183, seed=12, n_clones=3)
+    s, g = to_long_form(sim, n_libs=1, copy_from="reads")
+    s, g = s.drop(columns=["clone_id"]), g.drop(columns=["clone_id"])
+
+    def run():
+        sc = isc.scRT(s.copy(), g.copy(), clone_col=None, cn_prior_method="g1_clones", device="cpu")
+        sc._pert_model()
+        return sc
+    fast = run()
+    real = prep._block_layout
+    monkeypatch.setattr(prep, "_block_layout", lambda *a, **k: None)
+    slow = run()
+    monkeypatch.setattr(prep, "_block_layout", real)
+    pd.testing.assert_frame_equal(fast.cn_g1.reset_index(drop=True), slow.cn_g1.reset_index(drop=True))
+    a = fast.cn_s.sort_values(["cell_id", "chr", "start"]).reset_index(drop=True)
+    b = slow.cn_s.sort_values(["cell_id", "chr", "start"]).reset_index(drop=True)
+    assert a["cluster_id"].dtype == b["cluster_id"].dtype
+    np.testing.assert_array_equal(a["cluster_id"].to_numpy(), b["cluster_id"].to_numpy())
+    assert a["chr"].map(type).eq(str).all() and b["chr"].map(type).eq(str).all()

@@ -12,6 +12,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++20 tools/depth_probe.hip -o tools/depth_probe
 //   ./depth_probe [cells=1250] [bins=5451] [LT=54] [waves_per_cu=12] [iters=20] [spread=1] [swap=0]
 // spread: cell tiles placed spread x a tile apart (the footprint of a spread x larger shard);
+// subset (9th argument, > 0): only that many cell tiles launched over the whole allocation.
 // work (8th argument, > 0): the load-schedule experiment instead -- that many VALU operations per
 // bin between the loads and the stores, m / v loaded in the bin that uses them or a bin ahead.
 // swap: the workgroup -> tile order: 0 cell tiles fastest (the pass's), 1 bin tiles fastest,
@@ -238,6 +239,19 @@ int main(int argc, char** argv) {
   const float t2 = time_ms([&] { depth_stream<2><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, nwt, sink); }, iters);
   const float t3 = time_ms([&] { depth_stream<3><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, nwt, sink); }, iters);
   const int work = argc > 8 ? atoi(argv[8]) : 0;
+  // subset (9th argument, > 0): launch only the first `subset` cell tiles of the allocation (a
+  // small launch over a large footprint)
+  const int subset = argc > 9 ? atoi(argv[9]) : 0;
+  if (subset > 0 && subset < nwt) {
+    const int ns = subset, Ts = ns * nbt;
+    const double bytes_s = (double)ns * 64 * L * (6.0 + 24.0 * P);
+    const dim3 gs(swap >= 2 ? (Ts + 7) / 8 * 8 : Ts);
+    const float ts = time_ms([&] { depth_stream<1><<<gs, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, ns, sink); }, iters);
+    const float tf = time_ms([&] { depth_stream<1><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, nwt, sink); }, iters);
+    printf("subset: %d of %d cell tiles (cells %d, LT %d, order %d): %.4f ms %.3f TB/s | all %d tiles %.4f ms %.3f TB/s\n",
+           ns, nwt, N, LT, swap, ts, bytes_s / ts / 1e9, nwt, tf, bytes / tf / 1e9);
+    return 0;
+  }
   if (work > 0) {                         // the schedule experiment (work_stream), order 2
     const dim3 g1((nwt * nbt + 7) / 8 * 8);
     const float a0 = time_ms([&] { work_stream<0><<<g1, 64, lds>>>(x, code, z, m, v, L, ldn, LT, nwt, work, sink); }, iters);

@@ -15,6 +15,10 @@ if python -c "import sys; sys.exit(0 if float('$ms') < 3.1 else 1)"; then
               "1250 5451 54 12" "1250 5451 54 8" "20000 5451 18 12"; do
     timeout -k 5 60 ./tools/depth_probe $args 20 1 2 | tee -a gpurun_out/${TAG}_fastbox.log || exit 1
   done
+  for args in "10000 5451 54 12 20 1 2 0 20" "10000 5451 18 12 20 1 2 0 20" "10000 5451 18 12 20 1 2 0 80" \
+              "1250 5451 54 12 20 8 2" "1250 5451 6 12 20 1 2"; do
+    timeout -k 5 60 ./tools/depth_probe $args | tee -a gpurun_out/${TAG}_fastbox.log || exit 1
+  done
   for w in 256 512 1024; do
     for args in "1250 5451 54 12" "10000 5451 18 12"; do
       timeout -k 5 60 ./tools/depth_probe $args 20 1 2 $w | tee -a gpurun_out/${TAG}_fastbox.log || exit 1
@@ -22,4 +26,5 @@ if python -c "import sys; sys.exit(0 if float('$ms') < 3.1 else 1)"; then
   done
 else
   echo "slow box ($ms ms): no sweep" | tee -a gpurun_out/${TAG}_fastbox.log
+  timeout -k 5 60 ./tools/depth_probe 10000 5451 54 12 20 1 2 0 20 | tee -a gpurun_out/${TAG}_fastbox.log || exit 1
 fi

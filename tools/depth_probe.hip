@@ -13,6 +13,7 @@
 //   ./depth_probe [cells=1250] [bins=5451] [LT=54] [waves_per_cu=12] [iters=20] [spread=1] [swap=0]
 // spread: cell tiles placed spread x a tile apart (the footprint of a spread x larger shard);
 // subset (9th argument, > 0): only that many cell tiles launched over the whole allocation.
+// layout (10th: 0 three hipMallocs, 1 one allocation) with pads m-z / v-m (11th / 12th, KB).
 // work (8th argument, > 0): the load-schedule experiment instead -- that many VALU operations per
 // bin between the loads and the stores, m / v loaded in the bin that uses them or a bin ahead.
 // swap: the workgroup -> tile order: 0 cell tiles fastest (the pass's), 1 bin tiles fastest,
@@ -212,9 +213,22 @@ int main(int argc, char** argv) {
   const size_t nz = (size_t)(ldn / 64) * spread * L * P * 64;
   float *z, *m, *v, *x, *sink;
   uint16_t* code;
-  CK(hipMalloc(&z, nz * 4));
-  CK(hipMalloc(&m, nz * 4));
-  CK(hipMalloc(&v, nz * 4));
+  // layout (10th-12th arguments): 0 = three hipMallocs (as the shard's torch tensors get them);
+  // 1 = one allocation, m at z + nz + pad_m KB, v at m + nz + pad_v KB
+  const int layout = argc > 10 ? atoi(argv[10]) : 0;
+  const size_t pad_m = (argc > 11 ? (size_t)atoll(argv[11]) : 0) * 256;   // KB -> floats
+  const size_t pad_v = (argc > 12 ? (size_t)atoll(argv[12]) : 0) * 256;
+  float* big = nullptr;
+  if (layout == 1) {
+    CK(hipMalloc(&big, (3 * nz + pad_m + pad_v) * 4));
+    z = big;
+    m = z + nz + pad_m;
+    v = m + nz + pad_v;
+  } else {
+    CK(hipMalloc(&z, nz * 4));
+    CK(hipMalloc(&m, nz * 4));
+    CK(hipMalloc(&v, nz * 4));
+  }
   CK(hipMalloc(&x, (size_t)L * ldn * 4));
   CK(hipMalloc(&code, (size_t)L * ldn * 2));
   CK(hipMalloc(&sink, 64));
@@ -248,8 +262,9 @@ int main(int argc, char** argv) {
     const dim3 gs(swap >= 2 ? (Ts + 7) / 8 * 8 : Ts);
     const float ts = time_ms([&] { depth_stream<1><<<gs, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, ns, sink); }, iters);
     const float tf = time_ms([&] { depth_stream<1><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, nwt, sink); }, iters);
-    printf("subset: %d of %d cell tiles (cells %d, LT %d, order %d): %.4f ms %.3f TB/s | all %d tiles %.4f ms %.3f TB/s\n",
-           ns, nwt, N, LT, swap, ts, bytes_s / ts / 1e9, nwt, tf, bytes / tf / 1e9);
+    printf("subset: %d of %d cell tiles (cells %d, LT %d, order %d): %.4f ms %.3f TB/s | all %d tiles %.4f ms %.3f TB/s"
+           " [z %p m-z %td B v-m %td B]\n", ns, nwt, N, LT, swap, ts, bytes_s / ts / 1e9, nwt, tf, bytes / tf / 1e9,
+           (void*)z, (char*)m - (char*)z, (char*)v - (char*)m);
     return 0;
   }
   if (work > 0) {                         // the schedule experiment (work_stream), order 2
@@ -263,6 +278,7 @@ int main(int argc, char** argv) {
            work, N, LT, a0, bytes / a0 / 1e9, a1, bytes / a1 / 1e9, o0, o1);
     return 0;
   }
+  printf("[z %p m-z %td B v-m %td B] ", (void*)z, (char*)m - (char*)z, (char*)v - (char*)m);
   printf("spread %d swap %d cells %d bins %d LT %d tiles %d (%.2f rounds of %d x %d slots): depth1 %.4f ms %.3f TB/s | depth2 %.4f ms "
          "%.3f TB/s | depth3 %.4f ms %.3f TB/s (occupancy %d/%d/%d)\n",
          spread, swap, N, L, LT, nwt * nbt, (double)nwt * nbt / ((double)ncu * occ[0]), ncu, occ[0], t1, bytes / t1 / 1e9, t2,

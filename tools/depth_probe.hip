@@ -13,7 +13,8 @@
 //   ./depth_probe [cells=1250] [bins=5451] [LT=54] [waves_per_cu=12] [iters=20] [spread=1] [swap=0]
 // spread: cell tiles placed spread x a tile apart (the footprint of a spread x larger shard);
 // subset (9th argument, > 0): only that many cell tiles launched over the whole allocation.
-// layout (10th: 0 three hipMallocs, 1 one allocation) with pads m-z / v-m (11th / 12th, KB).
+// layout (10th: 0 three hipMallocs, 1 one allocation, 2 three hipDeviceMallocContiguous ones, 3 one
+// contiguous allocation) with pads m-z / v-m (11th / 12th, KB, layouts 1 and 3).
 // work (8th argument, > 0): the load-schedule experiment instead -- that many VALU operations per
 // bin between the loads and the stores, m / v loaded in the bin that uses them or a bin ahead.
 // swap: the workgroup -> tile order: 0 cell tiles fastest (the pass's), 1 bin tiles fastest,
@@ -219,11 +220,16 @@ int main(int argc, char** argv) {
   const size_t pad_m = (argc > 11 ? (size_t)atoll(argv[11]) : 0) * 256;   // KB -> floats
   const size_t pad_v = (argc > 12 ? (size_t)atoll(argv[12]) : 0) * 256;
   float* big = nullptr;
-  if (layout == 1) {
-    CK(hipMalloc(&big, (3 * nz + pad_m + pad_v) * 4));
+  if (layout == 1 || layout == 3) {
+    if (layout == 1) CK(hipMalloc(&big, (3 * nz + pad_m + pad_v) * 4));
+    else CK(hipExtMallocWithFlags((void**)&big, (3 * nz + pad_m + pad_v) * 4, hipDeviceMallocContiguous));
     z = big;
     m = z + nz + pad_m;
     v = m + nz + pad_v;
+  } else if (layout == 2) {                    // three physically contiguous allocations
+    CK(hipExtMallocWithFlags((void**)&z, nz * 4, hipDeviceMallocContiguous));
+    CK(hipExtMallocWithFlags((void**)&m, nz * 4, hipDeviceMallocContiguous));
+    CK(hipExtMallocWithFlags((void**)&v, nz * 4, hipDeviceMallocContiguous));
   } else {
     CK(hipMalloc(&z, nz * 4));
     CK(hipMalloc(&m, nz * 4));

@@ -14,7 +14,8 @@
 // spread: cell tiles placed spread x a tile apart (the footprint of a spread x larger shard);
 // subset (9th argument, > 0): only that many cell tiles launched over the whole allocation.
 // layout (10th: 0 three hipMallocs, 1 one allocation, 2 three hipDeviceMallocContiguous ones, 3 one
-// contiguous allocation) with pads m-z / v-m (11th / 12th, KB, layouts 1 and 3).
+// contiguous allocation) with pads m-z / v-m (11th / 12th, KB, layouts 1 and 3); alloc_cells
+// (13th): allocations sized for that many cells.
 // work (8th argument, > 0): the load-schedule experiment instead -- that many VALU operations per
 // bin between the loads and the stores, m / v loaded in the bin that uses them or a bin ahead.
 // swap: the workgroup -> tile order: 0 cell tiles fastest (the pass's), 1 bin tiles fastest,
@@ -211,7 +212,11 @@ int main(int argc, char** argv) {
   if (N <= 0 || L <= 0 || LT <= 0 || wpc <= 0 || wpc > 32 || spread < 1 || spread > 16) return 2;
   const int ldn = (N + 255) / 256 * 256;
   const int nwt = (N + 63) / 64;
-  const size_t nz = (size_t)(ldn / 64) * spread * L * P * 64;
+  // alloc_cells (13th argument): size the z / m / v allocations for that many cells (>= N), the
+  // tiles of the N cells at their start
+  const int alloc_cells = argc > 13 ? atoi(argv[13]) : N;
+  const size_t nz_used = (size_t)(ldn / 64) * spread * L * P * 64;
+  const size_t nz = alloc_cells > N ? (size_t)((alloc_cells + 255) / 256 * 4) * spread * L * P * 64 : nz_used;
   float *z, *m, *v, *x, *sink;
   uint16_t* code;
   // layout (10th-12th arguments): 0 = three hipMallocs (as the shard's torch tensors get them);

@@ -23,13 +23,27 @@ init = init_params(2, reads, np.zeros(cells, int), 1, 13, 4, ploidy=eta.argmax_s
 sh = PertShard(2, reads, data["gc"], np.zeros(cells, int), 1, 13, 4, init, eta=eta, lamb=0.75, beta_means=bm,
                device=dev, variant=int(os.environ.get("VARIANT", "2")), bins_per_tile=int(os.environ.get("LT", "0")))
 L = reads.shape[0]
-n_wg = (-(-cells // 64)) * (-(-L // sh.bins_per_tile))
-dbg = torch.zeros(n_wg * 4, dtype=torch.int64, device=dev)
+n_ct, n_bt = -(-cells // 64), -(-L // sh.bins_per_tile)
+n_wg = n_ct * n_bt
+order = int(os.environ.get("PERT_ENUM3_ORDER", "2"))
+n_slots = -(-n_wg // 8) * 8 if order >= 2 else n_wg        # the 1-D grid is rounded up to 8
+dbg = torch.zeros(n_slots * 4, dtype=torch.int64, device=dev)
 sh._state.g_pi = _ptr(dbg)
 for t in range(1, 8):
     sh._launch_step(t)
 torch.cuda.synchronize()
-d = dbg.cpu().numpy().reshape(n_wg, 4)
+d = dbg.cpu().numpy().reshape(n_slots, 4)
+# tile of each stamp row (row = workgroup index), padding rows (no tile) dropped
+i = np.arange(n_slots)
+if order >= 2:
+    per = -(-n_wg // 8)
+    w = (i % 8) * per + i // 8
+    row_wt, row_bt = (w // n_bt, w % n_bt) if order == 2 else (w % n_ct, w // n_ct)
+else:
+    row_wt, row_bt = i % n_ct, i // n_ct
+keep = d[:, 2] > 0
+d, row_wt, row_bt = d[keep], row_wt[keep], row_bt[keep]
+n_wg = int(keep.sum())
 t0 = d[:, 0].min()
 ent, first, ex = (d[:, 0] - t0) / 100.0, (d[:, 1] - t0) / 100.0, (d[:, 2] - t0) / 100.0   # microseconds
 span = ex.max()
@@ -57,9 +71,7 @@ if (~first_round).any():
         print("wave dur mid-kernel pct              :", q(dur[mid]))
 
 # where the slow waves are: by bin tile, by cell tile, by SIMD occupancy of their CU
-n_ct = -(-cells // 64)
-by = np.arange(n_wg) // n_ct
-wt = np.arange(n_wg) % n_ct
+by, wt = row_bt, row_wt
 hw = (d[:, 3] & 0xffffffff).astype(np.int64)
 simd = (hw >> 4) & 3
 cu = (hw >> 8) & 15

@@ -278,6 +278,31 @@ int main(int argc, char** argv) {
            (void*)z, (char*)m - (char*)z, (char*)v - (char*)m);
     return 0;
   }
+  // sets (14th argument, > 1): allocate that many z / m / v sets in one process (each held while
+  // the next is made) and time depth 1 on each: do some placements stream fast and others not?
+  const int sets = argc > 14 ? atoi(argv[14]) : 1;
+  if (sets > 1) {
+    printf("set 0 [z %p]: %.4f ms %.3f TB/s\n", (void*)z, t1, bytes / t1 / 1e9);
+    for (int si = 1; si < sets; ++si) {
+      float *z2, *m2, *v2;
+      if (layout == 2) {
+        CK(hipExtMallocWithFlags((void**)&z2, nz * 4, hipDeviceMallocContiguous));
+        CK(hipExtMallocWithFlags((void**)&m2, nz * 4, hipDeviceMallocContiguous));
+        CK(hipExtMallocWithFlags((void**)&v2, nz * 4, hipDeviceMallocContiguous));
+      } else {
+        CK(hipMalloc(&z2, nz * 4));
+        CK(hipMalloc(&m2, nz * 4));
+        CK(hipMalloc(&v2, nz * 4));
+      }
+      CK(hipMemset(z2, 0, nz * 4));
+      CK(hipMemset(m2, 0, nz * 4));
+      CK(hipMemset(v2, 0, nz * 4));
+      const float ts = time_ms([&] { depth_stream<1><<<grid, 64, lds>>>(x, code, z2, m2, v2, L, ldn, LT, spread, swap, nwt, sink); }, iters);
+      printf("set %d [z %p]: %.4f ms %.3f TB/s\n", si, (void*)z2, ts, bytes / ts / 1e9);
+      fflush(stdout);
+    }
+    return 0;
+  }
   if (work > 0) {                         // the schedule experiment (work_stream), order 2
     const dim3 g1((nwt * nbt + 7) / 8 * 8);
     const float a0 = time_ms([&] { work_stream<0><<<g1, 64, lds>>>(x, code, z, m, v, L, ldn, LT, nwt, work, sink); }, iters);

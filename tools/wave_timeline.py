@@ -97,3 +97,14 @@ for q in range(5):
 for q in range(5):
     m = (wt >= q * n_ct / 5) & (wt < (q + 1) * n_ct / 5)
     print("cell tiles quintile {}: dur mean {:.1f}".format(q, dur[m].mean()))
+
+# variance of the wave durations within a CU / SIMD against between CUs / XCDs (one-round launches:
+# does a wave's speed follow its CU, or is it the wave's own?)
+def _share(key):
+    _, idx = np.unique(key, return_inverse=True)
+    means = np.bincount(idx, dur) / np.bincount(idx)
+    return float(np.var(means[idx]) / np.var(dur))
+print("share of duration variance between XCDs {:.2f}, between CUs {:.2f}, between SIMDs {:.2f}".format(
+    _share(xcc), _share(cu_key), _share(simd_key)))
+if os.environ.get("DUMP"):
+    np.savez(os.environ["DUMP"], d=d, wt=wt, bt=by)

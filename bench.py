@@ -515,6 +515,9 @@ def main():
                 "kernel_frac_of_ceiling": ceil_ms / kern_ms,
                 "what": "pert_stream_ceiling: the pass's HBM streams (x, eta code, z/m/v read + written) with no "
                         "arithmetic, same tiles, same shard, same process"}
+            rec["roofline"]["pi_placement"] = dict(shard.placement or {"candidates_ms": None},
+                                                   what="PertShard.choose_pi_placement: pattern time of each "
+                                                        "z/m/v allocation tried at set-up (fastest kept)")
         if args.fit == "step2" and args.variant == 3 and shard.fused:
             rec["roofline"]["note"] = ("one launch per step (pert_enum_step): the pass with the reductions and "
                                        "Adam folded in; kernel_ms is that launch")

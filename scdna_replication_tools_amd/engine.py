@@ -21,6 +21,7 @@ from __future__ import annotations
 import ctypes
 import contextlib
 import math
+import os
 import threading
 from dataclasses import dataclass, field
 from typing import Callable, Dict, Optional
@@ -35,6 +36,21 @@ ADAM_EPS = 1e-8
 F32 = np.float32
 EPS32 = float(np.finfo(np.float32).eps)
 TINY32 = float(np.finfo(np.float32).tiny)
+
+# pi-state placement search (PertShard.choose_pi_placement): candidate z / m / v allocations per
+# shard (env PERT_PLACEMENT; 0 or 1 = the first allocation only), the smallest pi state searched
+# (fp32 elements: 1,250 cells x 5,451 bins x 13 states is 89 M), and the pattern rate (bytes/s) at
+# which a placement counts as fast and the search stops (MI355X: slow placements stream the
+# pass's pattern at 5.1-5.3 TB/s, fast ones at 5.9-6.3 TB/s; profiles/r05z_sets_probe.log)
+PLACEMENT_CANDIDATES = 24
+PLACEMENT_MIN_FLOATS = 32 * 1024 * 1024
+PLACEMENT_FAST_RATE = 5.8e12
+# each try past the first moves at least this far through free HBM (a small set is followed by a
+# held spacer), and the search holds at most PLACEMENT_MAX_HELD bytes of tries and spacers: the
+# slow placements come in runs of ~15-45 GB of allocations (r05ab, r05ac: the 3rd 8.7 GB set, the
+# 5th 4.4 GB set, the 6th-7th 2.2 GB set + spacer, the 10th-12th 1.1 GB set + spacer fast)
+PLACEMENT_STRIDE = 3 << 30
+PLACEMENT_MAX_HELD = 96 << 30
 
 
 # --------------------------------------------------------------------------- transforms
@@ -349,7 +365,8 @@ class PertShard:
                  is_root: bool = True, n_cells_total: Optional[int] = None,
                  allreduce: Optional[Callable[[torch.Tensor], None]] = None,
                  dirichlet_mode: str = "torch32", bins_per_tile: int = 0, variant: int = 3, fused: bool = False,
-                 paired: bool = False, lib=None, comm: Optional[RcclComm] = None):
+                 paired: bool = False, lib=None, comm: Optional[RcclComm] = None,
+                 placement: Optional[int] = None):
         self.lib = nat.lib() if lib is None else lib        # another build of the ABI (A/B tools)
         # the chunked SVI loop's handle: the product library through CDLL (the call releases the
         # GIL while it queues its launches); an A/B build keeps its own handle
@@ -515,6 +532,12 @@ class PertShard:
             bins_per_tile=self.bins_per_tile, variant=int(variant))
         self._hp = nat.PertAdamHparams(lr=self.lr, beta1=self.betas[0], beta2=self.betas[1], eps=self.eps,
                                        step_size=0.0, inv_bc2_sqrt=0.0)
+        self.placement = None        # the pi-state placement search's record (choose_pi_placement)
+        if placement is None:
+            placement = int(os.environ.get("PERT_PLACEMENT", str(PLACEMENT_CANDIDATES)))
+        if placement > 1 and self.z_pi is not None and self.variant == 3 and \
+                self.z_pi.numel() >= PLACEMENT_MIN_FLOATS:
+            self.choose_pi_placement(placement)
 
     # ------------------------------------------------------------------ layouts
     def _pad_rows(self, a: torch.Tensor, dev) -> torch.Tensor:
@@ -665,6 +688,77 @@ class PertShard:
             e1.record()
             e1.synchronize()
         return e0.elapsed_time(e1) / reps
+
+    def _set_pi_ptrs(self, z: torch.Tensor, m: torch.Tensor, v: torch.Tensor):
+        self._state.z_pi, self._state.m_pi, self._state.v_pi = _ptr(z), _ptr(m), _ptr(v)
+
+    def choose_pi_placement(self, candidates: int = PLACEMENT_CANDIDATES) -> dict:
+        """Pick where the pi state (z / m / v, 97 % of the pass's bytes) lives in HBM.
+
+        The pass's read-modify-write pattern streams at 5.1-5.3 TB/s from some physical
+        placements of the three arrays and at 5.9-6.3 TB/s from others; which one an allocation
+        gets is not selectable (relative offsets, contiguity and size make no difference:
+        DESIGN.md section 5), but it is fixed once allocated and measurable in a few passes'
+        time.  So: time pert_stream_ceiling (the pass's own streams on this shard's grid, values
+        written back unchanged) on the current arrays; while that is slower than
+        PLACEMENT_FAST_RATE, allocate another set (the earlier ones held, so it lands elsewhere)
+        and time it, up to ``candidates`` sets; move the state into the fastest and free the
+        rest.  Results do not depend on the placement (same data, same kernel).  Returns (and
+        keeps in ``self.placement``) the candidates' times and the choice."""
+        cells = -(-self.N // 64) * 64
+        pattern_bytes = float(cells) * self.L * (6.0 + 24.0 * self.P)
+        set_bytes = 3 * self.z_pi.numel() * 4
+
+        def timed() -> float:
+            s = self._stream()
+            with self._dev():
+                nat.check(self.lib.pert_stream_ceiling(ctypes.byref(self._prob), ctypes.byref(self._state), s),
+                          "pert_stream_ceiling")
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(2):
+                    nat.check(self.lib.pert_stream_ceiling(ctypes.byref(self._prob), ctypes.byref(self._state),
+                                                           s), "pert_stream_ceiling")
+                e1.record()
+                e1.synchronize()
+            return e0.elapsed_time(e1) / 2
+
+        first = (self.z_pi, self.m_pi, self.v_pi)
+        best, best_ms = first, timed()
+        times = [best_ms]
+        held = []
+        spacer = max(0, PLACEMENT_STRIDE - set_bytes)
+        held_bytes = 0
+        while len(times) < candidates and pattern_bytes / (best_ms * 1e-3) < PLACEMENT_FAST_RATE:
+            free, _ = torch.cuda.mem_get_info(self.device)
+            step = set_bytes + spacer
+            if free < step + set_bytes + (8 << 30) or held_bytes + step > PLACEMENT_MAX_HELD:
+                break
+            if spacer:
+                held.append(torch.empty(spacer, dtype=torch.uint8, device=self.device))
+            cand = tuple(torch.empty_like(self.z_pi) for _ in range(3))
+            held_bytes += step
+            self._set_pi_ptrs(*cand)
+            t = timed()
+            times.append(t)
+            if t < best_ms:
+                held.append(best)
+                best, best_ms = cand, t
+            else:
+                held.append(cand)
+        if best is not first:
+            for dst, src in zip(best, first):
+                dst.copy_(src)
+        self.z_pi, self.m_pi, self.v_pi = best
+        self._set_pi_ptrs(*best)
+        del held, first
+        if len(times) > 1:
+            torch.cuda.synchronize(self.device)
+            torch.cuda.empty_cache()             # the tries and spacers back to the device
+        self.placement = {"candidates_ms": [round(t, 4) for t in times], "chosen": times.index(best_ms),
+                          "pattern_tbs": round(pattern_bytes / (best_ms * 1e-3) / 1e12, 3)}
+        return self.placement
 
     def _finalize(self):
         """Reductions of the pass partials; with a process group, the shard's shared block is

@@ -21,6 +21,7 @@
 // swap: the workgroup -> tile order: 0 cell tiles fastest (the pass's), 1 bin tiles fastest,
 // 2 / 3 XCD-aware (XCD k gets a contiguous eighth of the tiles, bin- / cell-fastest).
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <cstdio>
 #include <cstdlib>
@@ -280,6 +281,18 @@ int main(int argc, char** argv) {
   }
   // sets (14th argument, > 1): allocate that many z / m / v sets in one process (each held while
   // the next is made) and time depth 1 on each: do some placements stream fast and others not?
+  // watch (15th argument, > 0): time the same set that many times, 20 ms apart (no new
+  // allocations): does one placement's speed change over time?
+  const int watch = argc > 15 ? atoi(argv[15]) : 0;
+  if (watch > 0) {
+    for (int w = 0; w < watch; ++w) {
+      const float tw = time_ms([&] { depth_stream<1><<<grid, 64, lds>>>(x, code, z, m, v, L, ldn, LT, spread, swap, nwt, sink); }, 3);
+      printf("watch %d t=%d ms: %.4f ms %.3f TB/s\n", w, w * 20, tw, bytes / tw / 1e9);
+      fflush(stdout);
+      usleep(20000);
+    }
+    return 0;
+  }
   const int sets = argc > 14 ? atoi(argv[14]) : 1;
   if (sets > 1) {
     printf("set 0 [z %p]: %.4f ms %.3f TB/s\n", (void*)z, t1, bytes / t1 / 1e9);

@@ -51,6 +51,9 @@ PLACEMENT_FAST_RATE = 5.8e12
 # 5th 4.4 GB set, the 6th-7th 2.2 GB set + spacer, the 10th-12th 1.1 GB set + spacer fast)
 PLACEMENT_STRIDE = 3 << 30
 PLACEMENT_MAX_HELD = 96 << 30
+# tries past the first fast one (fast placements come at two rates, ~6.0 and ~6.3 TB/s:
+# r05z 10 k sets 2.76-2.97 ms)
+PLACEMENT_EXTRA = 2
 
 
 # --------------------------------------------------------------------------- transforms
@@ -702,8 +705,8 @@ class PertShard:
         time.  So: time pert_stream_ceiling (the pass's own streams on this shard's grid, values
         written back unchanged) on the current arrays; while that is slower than
         PLACEMENT_FAST_RATE, allocate another set (the earlier ones held, so it lands elsewhere)
-        and time it, up to ``candidates`` sets; move the state into the fastest and free the
-        rest.  Results do not depend on the placement (same data, same kernel).  Returns (and
+        and time it, up to ``candidates`` sets, and PLACEMENT_EXTRA more once one is fast (fast
+        placements come at two rates); move the state into the fastest and free the rest.  Results do not depend on the placement (same data, same kernel).  Returns (and
         keeps in ``self.placement``) the candidates' times and the choice."""
         cells = -(-self.N // 64) * 64
         pattern_bytes = float(cells) * self.L * (6.0 + 24.0 * self.P)
@@ -730,7 +733,12 @@ class PertShard:
         held = []
         spacer = max(0, PLACEMENT_STRIDE - set_bytes)
         held_bytes = 0
-        while len(times) < candidates and pattern_bytes / (best_ms * 1e-3) < PLACEMENT_FAST_RATE:
+        fast_at = None                           # the try that first streamed fast
+        while len(times) < candidates:
+            if fast_at is None and pattern_bytes / (best_ms * 1e-3) >= PLACEMENT_FAST_RATE:
+                fast_at = len(times)
+            if fast_at is not None and len(times) >= fast_at + PLACEMENT_EXTRA:
+                break
             free, _ = torch.cuda.mem_get_info(self.device)
             step = set_bytes + spacer
             if free < step + set_bytes + (8 << 30) or held_bytes + step > PLACEMENT_MAX_HELD:

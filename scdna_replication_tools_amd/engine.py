@@ -358,6 +358,43 @@ def _ptr(t: Optional[torch.Tensor]) -> int:
     return 0 if t is None else int(t.data_ptr())
 
 
+def placement_search(first, time_set: Callable, alloc: Callable, free_bytes: Callable, set_bytes: int,
+                     pattern_bytes: float, candidates: int = PLACEMENT_CANDIDATES):
+    """The loop of PertShard.choose_pi_placement, apart from the device: ``time_set(s)`` times
+    the pass's stream pattern on set s (ms), ``alloc(spacer)`` returns a new set and the spacer
+    allocations made before it, ``free_bytes()`` the device's free memory.  Tries sets while
+    the best streams below PLACEMENT_FAST_RATE, then PLACEMENT_EXTRA more, within
+    ``candidates`` tries, PLACEMENT_MAX_HELD bytes held and 8 GB left free.  Returns the
+    fastest set, every try's time (the first set's first) and the list of what was held
+    (for the caller to drop once the state has moved)."""
+    best = first
+    best_ms = time_set(first)
+    times = [best_ms]
+    held = []
+    spacer = max(0, PLACEMENT_STRIDE - set_bytes)
+    held_bytes = 0
+    fast_at = None                               # the try count when a fast set was first seen
+    while len(times) < candidates:
+        if fast_at is None and pattern_bytes / (best_ms * 1e-3) >= PLACEMENT_FAST_RATE:
+            fast_at = len(times)
+        if fast_at is not None and len(times) >= fast_at + PLACEMENT_EXTRA:
+            break
+        step = set_bytes + spacer
+        if free_bytes() < step + set_bytes + (8 << 30) or held_bytes + step > PLACEMENT_MAX_HELD:
+            break
+        cand, sp = alloc(spacer)
+        held.extend(sp)
+        held_bytes += step
+        t = time_set(cand)
+        times.append(t)
+        if t < best_ms:
+            held.append(best)
+            best, best_ms = cand, t
+        else:
+            held.append(cand)
+    return best, times, held
+
+
 class PertShard:
     """One fit (kind 1/2/3) over one contiguous cell shard, resident on one GPU."""
 
@@ -706,8 +743,10 @@ class PertShard:
         written back unchanged) on the current arrays; while that is slower than
         PLACEMENT_FAST_RATE, allocate another set (the earlier ones held, so it lands elsewhere)
         and time it, up to ``candidates`` sets, and PLACEMENT_EXTRA more once one is fast (fast
-        placements come at two rates); move the state into the fastest and free the rest.  Results do not depend on the placement (same data, same kernel).  Returns (and
-        keeps in ``self.placement``) the candidates' times and the choice."""
+        placements come at two rates); move the state into the fastest and free the rest
+        (``placement_search``).  Results do not depend on the placement (same data, same
+        kernel).  Returns (and keeps in ``self.placement``) the candidates' times and the
+        choice."""
         cells = -(-self.N // 64) * 64
         pattern_bytes = float(cells) * self.L * (6.0 + 24.0 * self.P)
         set_bytes = 3 * self.z_pi.numel() * 4
@@ -728,33 +767,18 @@ class PertShard:
             return e0.elapsed_time(e1) / 2
 
         first = (self.z_pi, self.m_pi, self.v_pi)
-        best, best_ms = first, timed()
-        times = [best_ms]
-        held = []
-        spacer = max(0, PLACEMENT_STRIDE - set_bytes)
-        held_bytes = 0
-        fast_at = None                           # the try that first streamed fast
-        while len(times) < candidates:
-            if fast_at is None and pattern_bytes / (best_ms * 1e-3) >= PLACEMENT_FAST_RATE:
-                fast_at = len(times)
-            if fast_at is not None and len(times) >= fast_at + PLACEMENT_EXTRA:
-                break
-            free, _ = torch.cuda.mem_get_info(self.device)
-            step = set_bytes + spacer
-            if free < step + set_bytes + (8 << 30) or held_bytes + step > PLACEMENT_MAX_HELD:
-                break
-            if spacer:
-                held.append(torch.empty(spacer, dtype=torch.uint8, device=self.device))
-            cand = tuple(torch.empty_like(self.z_pi) for _ in range(3))
-            held_bytes += step
+
+        def time_set(cand) -> float:
             self._set_pi_ptrs(*cand)
-            t = timed()
-            times.append(t)
-            if t < best_ms:
-                held.append(best)
-                best, best_ms = cand, t
-            else:
-                held.append(cand)
+            return timed()
+
+        def alloc(spacer: int):
+            held = [torch.empty(spacer, dtype=torch.uint8, device=self.device)] if spacer else []
+            return tuple(torch.empty_like(self.z_pi) for _ in range(3)), held
+
+        best, times, held = placement_search(first, time_set, alloc, lambda: torch.cuda.mem_get_info(self.device)[0],
+                                             set_bytes, pattern_bytes, candidates)
+        best_ms = min(times)
         if best is not first:
             for dst, src in zip(best, first):
                 dst.copy_(src)

@@ -253,3 +253,29 @@ def test_online_argmax_gradient_is_minus_the_others_sum(nat):
         # correction on 1 - pi_jmax alone showed up here as up to ~1,300 ulps (p99 ~22)
         assert np.percentile(ulps, 99) < 4.0, np.percentile(ulps, 99)
         assert ulps_mag.max() < 64.0, ulps_mag.max()
+
+
+@pytest.mark.parametrize("dlo,dhi", [(0.3, 1.3), (1.0, 1.6), (1.0, 5.0), (2.0, 7.0), (0.5, 12.0)])
+def test_online_low_coverage_matches_cellbin(nat, dlo, dhi):
+    """The low-coverage regime of the three-wave pass (D = u omega (1-lam)/lam below the
+    asymptotic threshold, as 20 kb bins put it: chains chi D < 1 clamped, 1 <= chi D < 5 shifted
+    -- two at a time in packed fp32 where both are -- and the rest asymptotic with the hoisted
+    invariants) against enum_cellbin's per-chain nb_lgdiff: the same E and pi-logit gradient
+    within fp32 rounding.  Counts 0..12 (zeros included), weak and strong prior rows."""
+    P, n = 13, 20000
+    rng = np.random.default_rng(11)
+    x = rng.integers(0, 13, n).astype(np.float32)
+    em1 = np.where(rng.random((n, P)) < 0.5, 0.0, rng.uniform(0, 5, (n, P))).astype(np.float32)
+    st = rng.integers(0, P, n)
+    strong = rng.random(n) < 0.5
+    em1[np.arange(n)[strong], st[strong]] = np.float32(1e6 - 1)
+    S1 = em1.sum(1)
+    z = rng.normal(size=(n, P)).astype(np.float32)
+    D = rng.uniform(dlo, dhi, n).astype(np.float32)
+    phi = rng.uniform(0.01, 0.99, n).astype(np.float32)
+    fwd = nat.selftest_enum_cellbin_host(P, x, em1, S1, z, np.log1p(-0.75), D, phi)
+    onl = nat.selftest_enum_online_host(P, x, em1, S1, z, np.log1p(-0.75), D, phi)
+    scale = np.maximum(1.0, np.abs(fwd["E"]))
+    assert (np.abs(onl["E"] - fwd["E"]) / scale).max() < 1e-5
+    g_scale = np.maximum(1.0, np.abs(fwd["gz"]).max(1, keepdims=True))
+    assert (np.abs(onl["gz"] - fwd["gz"]) / g_scale).max() < 1e-5

@@ -53,8 +53,8 @@ def assign_s_to_clones(s_phase_cells: pd.DataFrame, clone_df: pd.DataFrame, col_
                                       clone_df.index.get_level_values(1)])
     li = cidx.get_indexer(pd.MultiIndex.from_arrays([piv.loci_chr.astype(str), piv.loci_start]))
     prof = clone_df.to_numpy(np.float64)
-    best = []
-    for n in range(piv.values.shape[1]):
+
+    def cell_r(n):
         v = piv.values[:, n]
         ok = (li >= 0) & np.isfinite(v)
         x = v[ok]
@@ -64,10 +64,32 @@ def assign_s_to_clones(s_phase_cells: pd.DataFrame, clone_df: pd.DataFrame, col_
         xc = x - x.mean()
         Yc = Y - Y.mean(0)
         with np.errstate(invalid="ignore", divide="ignore"):
-            r = (xc @ Yc) / (np.linalg.norm(xc) * np.linalg.norm(Yc, axis=0))
+            return (xc @ Yc) / (np.linalg.norm(xc) * np.linalg.norm(Yc, axis=0))
+
+    def pick(r):
         # Series.argmax (:71): first maximum, NaN skipped; all NaN (a constant profile) gives
         # -1 in the pandas the reference ran on, i.e. the last clone
-        best.append(clone_df.columns[int(np.nanargmax(r)) if np.isfinite(r).any() else -1])
+        return int(np.nanargmax(r)) if np.isfinite(r).any() else -1
+
+    n_cells = piv.values.shape[1]
+    picks = None
+    if n_cells and np.all(li >= 0) and np.isfinite(prof).all() and np.isfinite(piv.values).all() and prof.shape[1] > 1:
+        # every cell shares every locus: all correlations as one product; a cell whose top two
+        # are within 1e-9 (relative) of each other, or any non-finite r, takes the per-cell
+        # arithmetic above, so the picks are the per-cell loop's
+        Y = prof[li]
+        Yc = Y - Y.mean(0)
+        X = piv.values
+        Xc = X - X.mean(0)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            R = (Xc.T @ Yc) / (np.linalg.norm(Xc, axis=0)[:, None] * np.linalg.norm(Yc, axis=0)[None, :])
+        top2 = np.sort(R, axis=1)[:, -2:]
+        close = ~np.isfinite(R).all(axis=1) | (np.abs(top2[:, 1] - top2[:, 0]) <= 1e-9 * np.abs(top2[:, 1]))
+        picks = np.argmax(R, axis=1)
+        for n in np.flatnonzero(close):
+            picks[n] = pick(cell_r(n))
+    best = [clone_df.columns[int(p)] for p in picks] if picks is not None else \
+        [clone_df.columns[pick(cell_r(n))] for n in range(n_cells)]
     if row_cell is not None:
         # the per-cell labels' dtype as infer_objects finds it for the rows (the same set of
         # values), then one gather per row

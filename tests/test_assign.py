@@ -188,3 +188,21 @@ def test_assign_block_table_integer_column_in_float64():
         ref = _ref_assign(s.copy(), prof.copy(), col_name="reads")
         got = assign_s_to_clones(s.copy(), prof.copy(), col_name="reads")
     assert (got["clone_id"].to_numpy() == ref["clone_id"].to_numpy()).all()
+
+
+def test_assign_all_shared_loci_product_path_near_ties():
+    """Every cell on every profile locus, no missing values: the correlations come from one
+    matrix product; clones within 1e-9 of each other (a near-duplicate listed later) take the
+    per-cell arithmetic, so the picks are the reference loop's."""
+    from scdna_replication_tools_amd import prep
+    rng = np.random.default_rng(31)
+    ids = ["A", "B", "C", "D"]
+    loci = _loci()
+    prof = _clones(ids, loci, rng)
+    prof["D"] = prof["A"] + rng.normal(0, 1e-8, len(loci))               # near-ties with A (r within ~1e-9)
+    s = _cells(prof, loci, 60, rng, ids[:3], inf_nan=False)
+    s = s.sort_values(["cell_id", "chr", "start"], kind="stable").reset_index(drop=True)
+    s["cell_id"] = s["cell_id"].map({c: c for c in s["cell_id"].unique()})
+    assert prep._block_layout(s, "cell_id", "chr", "start", "copy") is not None
+    _compare(s, prof)
+    _compare(s.sample(frac=1.0, random_state=1).reset_index(drop=True), prof)   # the general pivot

@@ -781,24 +781,33 @@ def _group_median(group: np.ndarray, values: np.ndarray, n_groups: int) -> np.nd
 
 def _consensus_blocks(cn: pd.DataFrame, col_name: str, clone_col: str, cn_state_col, keys: "RegularKeys"):
     """consensus_clone_profiles' medians on a regular sorted table (every cell one block of
-    the same L loci, one clone per cell): the (L, cells) matrix of ``col_name``, each cell's
-    modal state, each clone's majority ploidy (row counts are L per cell, so cell counts
-    decide), and per clone a column median over its kept cells.  (L, n_clones) and the
-    sorted clone ids, or None (NaN values or states, a cell in two clones: the general path)."""
+    the same L loci, one clone per cell): ``consensus_arrays`` on its columns.  (L,
+    n_clones) and the sorted clone ids, or None (the general path)."""
     B, L = keys.cells.size, keys.regular
-    clone = cn[clone_col].to_numpy()
+    return consensus_arrays(cn[clone_col].to_numpy(), cn[col_name].to_numpy(np.float64),
+                            None if cn_state_col is None else cn[cn_state_col].to_numpy(), B, L)
+
+
+def consensus_arrays(clone: np.ndarray, values: np.ndarray, states: Optional[np.ndarray], B: int, L: int):
+    """The medians of compute_consensus_clone_profiles (:42-88) for a table of B per-cell
+    blocks of the same L loci (rows b L .. b L + L - 1 are cell b's, in one locus order): each
+    cell's modal state, each clone's majority ploidy (row counts are L per cell, so cell counts
+    decide), and per clone a column median over its kept cells.  Neither the order of the cells
+    nor that of the loci matters (medians and counts); rows come out in the blocks' locus order.
+    (L, n_clones) and the sorted clone ids, or None (NaN values or states, a cell in two
+    clones: the general path)."""
     if clone.size != B * L or not _constant_rows(clone, B, L):
         return None
     kcell, ku = _sorted_codes(clone[::L])
     if "None" in set(ku.tolist()):                       # clone 'None' is removed (:63)
         bad = int(np.flatnonzero(ku == "None")[0])
         kcell = np.where(kcell == bad, -1, kcell)
-    vals = cn[col_name].to_numpy(np.float64).reshape(B, L)
+    vals = np.asarray(values, dtype=np.float64).reshape(B, L)
     if np.isnan(vals).any():
         return None
     keep = kcell >= 0
-    if cn_state_col is not None:
-        st = cn[cn_state_col].to_numpy().reshape(B, L)
+    if states is not None:
+        st = np.asarray(states).reshape(B, L)
         if st.dtype.kind not in "iu":
             if st.dtype.kind != "f" or np.isnan(st).any() or not (st == np.floor(st)).all():
                 return None

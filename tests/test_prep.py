@@ -384,3 +384,25 @@ def test_clone_prior_of_a_cell_range_equals_the_whole_prior_sliced():
         w = m._build_etas(inp, profiles)
         p = m._build_etas(inp, profiles, cells=slice(3, 17))
         np.testing.assert_array_equal(p.dense(), w.dense()[:, 3:17], err_msg=method)
+
+
+def test_scrt_consensus_block_path_any_block_and_locus_order():
+    """The consensus from the table's blocks as they lie (cells in any order, every block's loci
+    in one shared but unsorted order, a clone 'None' cell): the general path's profiles exactly."""
+    from scdna_replication_tools_amd.infer_scRT import consensus_profiles
+    from scdna_replication_tools_amd.simulator import simulate, to_long_form
+    sim = simulate(n_s=4, n_g=60, n_bins=400, num_reads=400 * 183, seed=9, n_clones=3)
+    _, df_g = to_long_form(sim, n_libs=1, copy_from="reads")
+    B = df_g["cell_id"].nunique()
+    L = len(df_g) // B
+    rng = np.random.default_rng(2)
+    cell_perm, locus_perm = rng.permutation(B), rng.permutation(L)
+    order = (cell_perm[:, None] * L + locus_perm[None, :]).reshape(-1)
+    df = df_g.iloc[order].reset_index(drop=True)
+    first = df["cell_id"].to_numpy()[0]
+    df.loc[df["cell_id"] == first, "clone_id"] = "None"
+    assert prep._block_layout(df, "cell_id", "chr", "start", None) is not None
+    for col in ("copy", "state"):
+        a = prep.consensus_clone_profiles(df, col, clone_col="clone_id", cn_state_col="state")
+        b = consensus_profiles(df, col, clone_col="clone_id", cn_state_col="state")
+        pd.testing.assert_frame_equal(a, b)

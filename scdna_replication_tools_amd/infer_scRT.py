@@ -109,18 +109,11 @@ def consensus_profiles(cn_g1: pd.DataFrame, col_name, clone_col='clone_id', cell
     the consensus' block path (no per-row hashing of the labels, identical result)."""
     lay = prep._block_layout(cn_g1, cell_col, chr_col, start_col, None)
     if lay is not None and cn_state_col is not None and cn_state_col in cn_g1.columns:
-        B, L, bp, q, ch0 = lay
-        fast = prep.consensus_arrays(cn_g1[clone_col].to_numpy(), cn_g1[col_name].to_numpy(np.float64),
-                                     cn_g1[cn_state_col].to_numpy(), B, L)
-        if fast is not None:
-            # the medians straight from the table's blocks (cells in table order, loci in the
-            # blocks' order, then sorted by q): no sorted copy of the table
-            med, ku = fast
-            chr_lab = pd.Categorical(np.array(prep.CHR_ORDER, dtype=object)[ch0[q]], categories=prep.CHR_ORDER)
-            idx = pd.MultiIndex.from_arrays([chr_lab, cn_g1[start_col].to_numpy()[:L][q]], names=[chr_col, start_col])
-            prof = pd.DataFrame(med[q], index=idx, columns=pd.Index(ku, name=clone_col))
-            prof = prof.dropna(how="all").dropna(axis=1, how="all").sort_index()
-        else:
+        L = lay[1]
+        # the medians straight from the table's blocks: no sorted copy of the table
+        prof = prep.consensus_from_blocks(cn_g1, lay, col_name, clone_col=clone_col, chr_col=chr_col,
+                                          start_col=start_col, cn_state_col=cn_state_col)
+        if prof is None:
             out, keys, _, _ = prep._block_table(cn_g1, lay, None, col_name, cn_state_col, cell_col, chr_col, start_col)
             prof = prep.consensus_clone_profiles(out, col_name, clone_col=clone_col, cell_col=cell_col,
                                                  chr_col=chr_col, start_col=start_col, cn_state_col=cn_state_col,

@@ -219,15 +219,43 @@ class pert_infer_scRT():
         self.iters = {}
         self._inp = None
 
+    # the input tables: after _prepare, their sorted copies -- possibly still being built on a
+    # background thread (prep.DeferredTable), in which case reading the attribute waits for it;
+    # the priors take per-cell labels from the raw attribute without waiting (_raw_table)
+    @property
+    def cn_s(self):
+        if isinstance(self._cn_s, prep.DeferredTable):
+            self._cn_s = self._cn_s.result()
+        return self._cn_s
+
+    @cn_s.setter
+    def cn_s(self, v):
+        self._cn_s = v
+
+    @property
+    def cn_g1(self):
+        if isinstance(self._cn_g1, prep.DeferredTable):
+            self._cn_g1 = self._cn_g1.result()
+        return self._cn_g1
+
+    @cn_g1.setter
+    def cn_g1(self, v):
+        self._cn_g1 = v
+
+    def _raw_table(self, which: str):
+        return self._cn_s if which == "s" else self._cn_g1
+
     # ------------------------------------------------------------------ prep (host)
-    def _prepare(self, on_g1_sorted=None) -> prep.PertInputs:
+    def _prepare(self, on_g1_sorted=None, defer_sorted: bool = False) -> prep.PertInputs:
         """pert_model.py:133-191, vectorised (prep.process_input_data): sorts and filters
-        self.cn_s / self.cn_g1 like the reference and returns the tensor inputs."""
+        self.cn_s / self.cn_g1 like the reference and returns the tensor inputs.
+        ``defer_sorted``: the sorted copies of per-cell-block tables are built on a background
+        thread (run_pert_model: the fit starts from the pivots; packaging takes the copies)."""
         if self._inp is None:
             self.cn_s, self.cn_g1, inp = prep.process_input_data(
-                self.cn_s, self.cn_g1, input_col=self.input_col, gc_col=self.gc_col, cell_col=self.cell_col,
+                self._cn_s, self._cn_g1, input_col=self.input_col, gc_col=self.gc_col, cell_col=self.cell_col,
                 library_col=self.library_col, chr_col=self.chr_col, start_col=self.start_col,
-                cn_state_col=self.cn_state_col, on_g1_sorted=on_g1_sorted)
+                cn_state_col=self.cn_state_col, on_g1_sorted=on_g1_sorted, defer_sorted=defer_sorted)
             self.L = len(inp.library_ids)
             self._inp = inp
         return self._inp
@@ -354,7 +382,7 @@ class pert_infer_scRT():
         if m == 'hmmcopy':
             return prep.build_cn_prior(inp.states_s[:, sl], w, P)
         if m == 'g1_clones':
-            return self._clone_prior(self.cn_s, inp.cells_s, profiles, keys=inp.keys_s, cell_range=cells)
+            return self._clone_prior(self._raw_table("s"), inp.cells_s, profiles, keys=inp.keys_s, cell_range=cells)
         if m == 'diploid':
             return prep.diploid_prior(L, sl.stop - sl.start, w, P)
         if m not in ('g1_cells', 'g1_composite'):
@@ -498,7 +526,8 @@ class pert_infer_scRT():
             helper.submit(CanonicalPiBlock.precompute, P, self.learning_rate, self.max_iter_step1 + 1)
             fut_prof = []
             tic = time.perf_counter()
-            inp = self._prepare(on_g1_sorted=lambda t, k: fut_prof.append(helper.submit(on_device, consensus, t, k)))
+            inp = self._prepare(on_g1_sorted=lambda t, k: fut_prof.append(helper.submit(on_device, consensus, t, k)),
+                                defer_sorted=True)
             if not fut_prof:                       # inputs prepared before this call: consensus now
                 fut_prof.append(helper.submit(on_device, consensus, self.cn_g1, inp.keys_g))
             n_libs = self.L
@@ -560,6 +589,12 @@ class pert_infer_scRT():
             s2 = self._shard(KIND_STEP2, dd, inp.reads_s, inp.libs_s, init2, eta=etas, lamb=float(lambda_fit[0]),
                              beta_means=beta_means_fit)
             mark("init_shard2")
+            # the sorted copies of the input tables (packaging's) are built while step 2 runs in
+            # the library (the fit thread waits in one GIL-free call): not beside the host work
+            # before it, whose interpreter time they would take
+            for t in (self._raw_table("s"), self._raw_table("g")):
+                if isinstance(t, prep.DeferredTable):
+                    t.start()
             logging.info('STEP 2: Jointly infer replication and CN states in high variance cells.')
             losses_s = self._svi(s2, self.max_iter, self.min_iter, "step2")
             mark("step2")
@@ -618,7 +653,7 @@ class pert_infer_scRT():
         stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
         ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
         with ctx:
-            etas2 = self._clone_prior(self.cn_g1, inp.cells_g, profiles, keys=inp.keys_g, cell_range=cells)
+            etas2 = self._clone_prior(self._raw_table("g"), inp.cells_g, profiles, keys=inp.keys_g, cell_range=cells)
             t0 = time.perf_counter()
             reads = inp.reads_g if cells is None else inp.reads_g[:, cells]
             t_init2, _, _ = self._guess_times(reads, etas2.argmax_states())

@@ -477,6 +477,17 @@ def _align(p: Pivot, chr_, start) -> Pivot:
 def _cell_libraries(cn: pd.DataFrame, keys: TableKeys, library_col: str, cells: np.ndarray):
     """(cell, library) pairs of get_libraries_tensor (:206-225) from the integer keys:
     the library labels in first-appearance order and one label per pivot cell."""
+    if isinstance(keys, RegularKeys) and isinstance(cn, DeferredTable):
+        # the source's blocks (constant within a block in any row order), heads in sorted order
+        B, L = keys.cells.size, keys.regular
+        v = cn.source[library_col].to_numpy()
+        if v.size == B * L and _constant_rows(v, B, L):
+            per_cell = cn.column_at(library_col, np.arange(B, dtype=np.int64) * L)
+            if not pd.isna(per_cell).any():
+                ids = list(pd.unique(per_cell))          # first appearance over the sorted rows
+                lab = pd.Series(per_cell, index=pd.Index(keys.cells)).reindex(np.asarray(cells)).to_numpy()
+                return ids, lab
+        cn = cn.result()
     if isinstance(keys, RegularKeys):
         # one label per cell block (else the general path below finds and refuses the cell
         # with two libraries)
@@ -515,11 +526,13 @@ def _cell_libraries(cn: pd.DataFrame, keys: TableKeys, library_col: str, cells: 
 
 def process_input_data(cn_s: pd.DataFrame, cn_g1: pd.DataFrame, input_col="reads", gc_col="gc",
                        cell_col="cell_id", library_col="library_id", chr_col="chr", start_col="start",
-                       cn_state_col="state", on_g1_sorted=None):
+                       cn_state_col="state", on_g1_sorted=None, defer_sorted: bool = False):
     """pert_model.py:133-191 (the unused rt prior aside).  Returns the sorted,
     NaN-filtered long tables and a ``PertInputs``.  ``on_g1_sorted(table, keys)`` is called
     with the sorted G1/2 table as soon as it exists (work that needs only it can start while
-    the S table is still being prepared)."""
+    the S table is still being prepared).  ``defer_sorted``: a per-cell-block table's sorted
+    copy comes back as a DeferredTable built on a background thread (the pivots, keys, library
+    index and gc are made without it)."""
     from concurrent.futures import ThreadPoolExecutor
 
     def table(cn, hook=None):
@@ -527,7 +540,8 @@ def process_input_data(cn_s: pd.DataFrame, cn_g1: pd.DataFrame, input_col="reads
         # passes release the GIL; the object-column passes interleave)
         lay = _block_layout(cn, cell_col, chr_col, start_col, input_col)
         if lay is not None:
-            return _block_table(cn, lay, hook, input_col, cn_state_col, cell_col, chr_col, start_col)
+            return _block_table(cn, lay, hook, input_col, cn_state_col, cell_col, chr_col, start_col,
+                                defer=defer_sorted)
         cn, k = _sorted_table(cn, cell_col, chr_col, start_col, notna_col=input_col)
         if hook is not None:
             hook(cn, k)
@@ -554,8 +568,14 @@ def process_input_data(cn_s: pd.DataFrame, cn_g1: pd.DataFrame, input_col="reads
     assert libs_s.shape[0] == ps_r.values.shape[1] and libs_g.shape[0] == pg_r.values.shape[1]
 
     # gc per locus: first row of each locus in the sorted S table
-    gcv = cn_s[gc_col].to_numpy(np.float64)
-    if getattr(ks, "regular", 0) and gcv.size == _n_rows(ks):
+    if isinstance(cn_s, DeferredTable):
+        gc_locus = cn_s.column_at(gc_col, np.arange(ks.regular)).astype(np.float64)   # cell 0's rows
+        gcv = None
+    else:
+        gcv = cn_s[gc_col].to_numpy(np.float64)
+    if gcv is None:
+        pass
+    elif getattr(ks, "regular", 0) and gcv.size == _n_rows(ks):
         gc_locus = gcv[:ks.regular]                      # regular table: cell 0's rows, locus order
     else:
         okr = ks.valid
@@ -633,7 +653,60 @@ def pivot_any(cn: pd.DataFrame, value_col: str, cell_col: str, chr_col: str, sta
     return Pivot(cells, np.array(CHR_ORDER, dtype=object)[ch0[q]], cn[start_col].to_numpy()[:L][q], vals)
 
 
-def _block_table(cn, lay, hook, input_col, cn_state_col, cell_col, chr_col, start_col):
+_DEFER_POOL = None
+_DEFER_LOCK = __import__("threading").Lock()
+
+
+def _defer_pool():
+    global _DEFER_POOL
+    with _DEFER_LOCK:
+        if _DEFER_POOL is None:
+            from concurrent.futures import ThreadPoolExecutor
+            _DEFER_POOL = ThreadPoolExecutor(max_workers=2, thread_name_prefix="pert-sort")
+        return _DEFER_POOL
+
+
+class DeferredTable:
+    """The sorted copy of a per-cell-block table (sort_by_cell_and_loci, pert_model.py:194-203),
+    built on a background thread once ``start()`` is called (or on first ``result()``): the fit
+    needs only the pivots to start, packaging needs the copy seconds later.  ``result()`` waits for it; ``column_at(name, rows)`` reads a column at
+    rows of the sorted order straight from the source table (sorted row r is the source's row
+    bp[r // L] L + q[r % L]), so the per-cell labels the priors and the library index take from
+    a cell's first row need no copy."""
+
+    def __init__(self, source: pd.DataFrame, lay, build):
+        self.source = source
+        self.lay = lay
+        self._build = build
+        self._fut = None
+        self._lock = __import__("threading").Lock()
+
+    def start(self) -> "DeferredTable":
+        """Begin the copy on the background thread (a fit starts it once its own host work is
+        done: the copy's object columns hold the interpreter lock for much of their time)."""
+        with self._lock:
+            if self._fut is None:
+                self._fut = _defer_pool().submit(self._build)
+        return self
+
+    def __len__(self) -> int:
+        return self.lay[0] * self.lay[1]
+
+    def result(self) -> pd.DataFrame:
+        return self.start()._fut.result()
+
+    def column_at(self, name: str, rows: np.ndarray) -> np.ndarray:
+        B, L, bp, q, _ = self.lay
+        rows = np.asarray(rows, dtype=np.int64)
+        return self.source[name].to_numpy()[bp[rows // L].astype(np.int64) * L + q[rows % L]]
+
+
+def resolved(cn):
+    """The table itself (a DeferredTable's sorted copy, once built)."""
+    return cn.result() if isinstance(cn, DeferredTable) else cn
+
+
+def _block_table(cn, lay, hook, input_col, cn_state_col, cell_col, chr_col, start_col, defer: bool = False):
     """process_input_data's per-table work for a per-cell-block table (_block_layout): the
     table sorted by (cell, chr, start) with one gather per column (the cell and chromosome
     columns rebuilt from the block heads), RegularKeys, and the two pivots as transposes of
@@ -643,19 +716,22 @@ def _block_table(cn, lay, hook, input_col, cn_state_col, cell_col, chr_col, star
     chq = ch0[q]
     loci_chr = np.array(CHR_ORDER, dtype=object)[chq]
     loci_start = cn[start_col].to_numpy()[:L][q]
-    order = (bp.astype(np.int64)[:, None] * L + q[None, :]).reshape(-1)
-    chr_cat = pd.Categorical.from_codes(np.tile(chq.astype(np.int8), B), categories=CHR_ORDER)
-    replace = {cell_col: np.repeat(cells.astype(object), L), chr_col: chr_cat}
-    for name in cn.columns:
-        # per-cell label columns (library, clone): one object per block, by identity -- the
-        # block heads repeated instead of a gather of every row
-        if name in replace or name == cell_col or cn[name].dtype != object:
-            continue
-        a = np.ascontiguousarray(cn[name].to_numpy())
-        p2 = _object_pointers(a).reshape(B, L)
-        if (p2 == p2[:, :1]).all():
-            replace[name] = np.repeat(a[::L][bp], L)
-    out = _take_columns(cn, order, replace=replace)
+
+    def build():
+        order = (bp.astype(np.int64)[:, None] * L + q[None, :]).reshape(-1)
+        chr_cat = pd.Categorical.from_codes(np.tile(chq.astype(np.int8), B), categories=CHR_ORDER)
+        replace = {cell_col: np.repeat(cells.astype(object), L), chr_col: chr_cat}
+        for name in cn.columns:
+            # per-cell label columns (library, clone): one object per block, by identity -- the
+            # block heads repeated instead of a gather of every row
+            if name in replace or name == cell_col or cn[name].dtype != object:
+                continue
+            a = np.ascontiguousarray(cn[name].to_numpy())
+            p2 = _object_pointers(a).reshape(B, L)
+            if (p2 == p2[:, :1]).all():
+                replace[name] = np.repeat(a[::L][bp], L)
+        return _take_columns(cn, order, replace=replace)
+    out = DeferredTable(cn, lay, build) if defer else build()
     k = RegularKeys(cells, loci_chr, loci_start, L)
     if hook is not None:
         hook(out, k)
@@ -664,7 +740,7 @@ def _block_table(cn, lay, hook, input_col, cn_state_col, cell_col, chr_col, star
         v = cn[col].to_numpy()
         if v.dtype.kind == "f" and np.isnan(v).any():
             # missing values: pivot_table's NaN handling on the sorted table
-            return drop_incomplete_loci(pivot_cells_by_loci(out, col, cell_col, chr_col, start_col, k))
+            return drop_incomplete_loci(pivot_cells_by_loci(resolved(out), col, cell_col, chr_col, start_col, k))
         return Pivot(cells, loci_chr, loci_start, _block_pivot(v, B, L, bp, q))
     return out, k, pivot(input_col), pivot(cn_state_col)
 
@@ -862,12 +938,37 @@ def _column_median(vals: np.ndarray, rows: np.ndarray) -> np.ndarray:
     return out
 
 
+def consensus_from_blocks(cn: pd.DataFrame, lay, col_name: str, clone_col="clone_id", chr_col="chr",
+                          start_col="start", cn_state_col="state"):
+    """consensus_clone_profiles of a per-cell-block table (``lay`` from _block_layout) from its
+    blocks as they lie (``consensus_arrays``: the order of cells and loci does not matter), as
+    the sorted copy's block path returns it -- index (chr as CHR_ORDER categories, start), sorted
+    -- without the copy; None where the general path is needed."""
+    B, L, bp, q, ch0 = lay
+    fast = consensus_arrays(cn[clone_col].to_numpy(), cn[col_name].to_numpy(np.float64),
+                            None if cn_state_col is None else cn[cn_state_col].to_numpy(), B, L)
+    if fast is None:
+        return None
+    med, ku = fast
+    chr_lab = pd.Categorical(np.array(CHR_ORDER, dtype=object)[ch0[q]], categories=CHR_ORDER)
+    idx = pd.MultiIndex.from_arrays([chr_lab, cn[start_col].to_numpy()[:L][q]], names=[chr_col, start_col])
+    prof = pd.DataFrame(med[q], index=idx, columns=pd.Index(ku, name=clone_col))
+    return prof.dropna(how="all").dropna(axis=1, how="all").sort_index()
+
+
 def consensus_clone_profiles(cn: pd.DataFrame, col_name: str, clone_col="clone_id", cell_col="cell_id",
                              chr_col="chr", start_col="start", cn_state_col="state", keys=None) -> pd.DataFrame:
     """compute_consensus_clone_profiles (:42-88): median of ``col_name`` per (locus, clone)
     over the clone's majority-ploidy cells; index (chr, start) sorted as pivot_table sorts
     it, columns the sorted clone ids.  Integer codes, row masks and one lexsort; the long
-    table itself is never copied."""
+    table itself is never copied.  A DeferredTable is taken from its source's blocks
+    (``consensus_from_blocks``) when they qualify, else from its sorted copy."""
+    if isinstance(cn, DeferredTable):
+        prof = consensus_from_blocks(cn.source, cn.lay, col_name, clone_col=clone_col, chr_col=chr_col,
+                                     start_col=start_col, cn_state_col=cn_state_col)
+        if prof is not None:
+            return prof
+        cn = cn.result()
     if (isinstance(keys, RegularKeys) and _n_rows(keys) == len(cn)
             and isinstance(cn[chr_col].dtype, pd.CategoricalDtype)):
         fast = _consensus_blocks(cn, col_name, clone_col, cn_state_col, keys)
@@ -920,6 +1021,8 @@ def consensus_clone_profiles(cn: pd.DataFrame, col_name: str, clone_col="clone_i
 def first_clone(cn: pd.DataFrame, cells, cell_col="cell_id", clone_col="clone_id", keys=None) -> np.ndarray:
     """cn.loc[cn[cell]==id][clone].values[0] for every id (pert_model.py:289-290).
     ``keys``: the table's TableKeys (row order), to find first rows by cell code."""
+    if isinstance(cn, DeferredTable) and not (isinstance(keys, RegularKeys) and _n_rows(keys) == len(cn)):
+        cn = cn.result()
     if keys is not None and _n_rows(keys) == len(cn):
         if isinstance(keys, RegularKeys):
             rows = np.arange(keys.cells.size) * keys.regular          # each cell's first row
@@ -927,7 +1030,8 @@ def first_clone(cn: pd.DataFrame, cells, cell_col="cell_id", clone_col="clone_id
             ok = keys.cell_code >= 0
             _, first = np.unique(keys.cell_code[ok], return_index=True)
             rows = np.flatnonzero(ok)[first]
-        clone_of = cn[clone_col].to_numpy()[rows]                  # per keys.cells
+        clone_of = (cn.column_at(clone_col, rows) if isinstance(cn, DeferredTable)
+                    else cn[clone_col].to_numpy()[rows])              # per keys.cells
         pos = pd.Index(keys.cells).get_indexer(np.asarray(cells))
         out = np.empty(len(pos), dtype=object)
         out[pos >= 0] = clone_of[pos[pos >= 0]]

@@ -406,3 +406,37 @@ def test_scrt_consensus_block_path_any_block_and_locus_order():
         a = prep.consensus_clone_profiles(df, col, clone_col="clone_id", cn_state_col="state")
         b = consensus_profiles(df, col, clone_col="clone_id", cn_state_col="state")
         pd.testing.assert_frame_equal(a, b)
+
+
+def test_process_input_data_deferred_sorted_tables_equal_eager():
+    """defer_sorted (run_pert_model): the sorted copies of per-cell-block tables built on a
+    background thread -- the same inputs, library index and gc as the eager path, the same
+    sorted tables once resolved, and the per-cell labels (first_clone, libraries) and the
+    consensus read from the source blocks equal to those of the sorted copies."""
+    from scdna_replication_tools_amd.simulator import simulate, to_long_form
+    sim = simulate(n_s=20, n_g=30, n_bins=300, num_reads=300 * 183, seed=12, n_clones=3)
+    df_s, df_g = to_long_form(sim, n_libs=2)
+    rng = np.random.default_rng(3)
+    B = df_s["cell_id"].nunique()
+    L = len(df_s) // B
+    order = (rng.permutation(B)[:, None] * L + rng.permutation(L)[None, :]).reshape(-1)
+    df_s = df_s.iloc[order].reset_index(drop=True)                  # blocks and loci in another order
+    seen = {}
+    s1, g1, a = prep.process_input_data(df_s, df_g)
+    s2, g2, b = prep.process_input_data(df_s, df_g, defer_sorted=True,
+                                        on_g1_sorted=lambda t, k: seen.setdefault("g", (t, k)))
+    assert isinstance(s2, prep.DeferredTable) and isinstance(seen["g"][0], prep.DeferredTable)
+    for f in ("reads_s", "reads_g", "states_s", "states_g", "gc", "libs_s", "libs_g", "cells_s", "cells_g",
+              "loci_chr", "loci_start"):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+    assert a.library_ids == b.library_ids
+    for name, (x, y) in {"clone_id": (s1, s2), "library_id": (g1, g2)}.items():
+        rows = np.arange(len(x))[::7]
+        np.testing.assert_array_equal(x[name].to_numpy()[rows], y.column_at(name, rows))
+    np.testing.assert_array_equal(prep.first_clone(s1, a.cells_s, keys=a.keys_s),
+                                  prep.first_clone(s2, b.cells_s, keys=b.keys_s))
+    pa = prep.consensus_clone_profiles(g1, "state", keys=a.keys_g)
+    pb = prep.consensus_clone_profiles(seen["g"][0], "state", keys=seen["g"][1])
+    pd.testing.assert_frame_equal(pa, pb)
+    pd.testing.assert_frame_equal(s1, prep.resolved(s2))
+    pd.testing.assert_frame_equal(g1, prep.resolved(g2))

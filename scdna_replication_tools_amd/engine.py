@@ -23,6 +23,7 @@ import contextlib
 import math
 import os
 import threading
+import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, Optional
 
@@ -445,6 +446,9 @@ class PertShard:
         f32 = dict(dtype=torch.float32, device=dev)
         self.ldn = ldn = -(-NS // nat.BLOCK) * nat.BLOCK      # row stride: stored columns rounded up to 256
 
+        # set-up timeline (seconds since the constructor began, per phase): timings["init"]
+        _t0 = time.perf_counter()
+        self.init_timings = {}
         # ---- inputs (pert_model.py:133-191 layouts)
         self.reads = self._pad_rows(torch.as_tensor(np.ascontiguousarray(reads, dtype=F32)), dev)
         self.gcf = gc_features(gc, self.K).to(dev).contiguous()
@@ -489,6 +493,7 @@ class PertShard:
                 self.rho_fixed_t = torch.as_tensor(np.asarray(rho_fixed, dtype=F32).reshape(L), device=dev)
         self.lamb = lam_f
 
+        self.init_timings["inputs"] = round(time.perf_counter() - _t0, 4)
         # ---- packed parameters (include/pert_hip.h pert_layout)
         self.lay = nat.make_layout(L, N, self.K1, self.n_libs)
         lay = self.lay
@@ -521,6 +526,7 @@ class PertShard:
         self._loop_bufs = None       # run_svi's control word / records / pinned host copy (reused)
         self._ctl_init = None
 
+        self.init_timings["params"] = round(time.perf_counter() - _t0, 4)
         # ---- constants of the loss (added on the host, summed over ranks once)
         # (fp64 on the device, from the padded reads already there: zero columns add nothing; a
         # small shard on the host, where the device's first lgamma launch would cost more)
@@ -544,6 +550,7 @@ class PertShard:
             self.allreduce(c)
         self.const_total = float(c.item())
 
+        self.init_timings["constants"] = round(time.perf_counter() - _t0, 4)
         # ---- C structs
         self._prob = nat.PertProblem(
             kind=self.kind, L=L, N=N, P=self.P, K1=self.K1, n_libs=self.n_libs,
@@ -572,12 +579,14 @@ class PertShard:
             bins_per_tile=self.bins_per_tile, variant=int(variant))
         self._hp = nat.PertAdamHparams(lr=self.lr, beta1=self.betas[0], beta2=self.betas[1], eps=self.eps,
                                        step_size=0.0, inv_bc2_sqrt=0.0)
+        self.init_timings["structs"] = round(time.perf_counter() - _t0, 4)
         self.placement = None        # the pi-state placement search's record (choose_pi_placement)
         if placement is None:
             placement = int(os.environ.get("PERT_PLACEMENT", str(PLACEMENT_CANDIDATES)))
         if placement > 1 and self.z_pi is not None and self.variant == 3 and \
                 self.z_pi.numel() >= PLACEMENT_MIN_FLOATS:
             self.choose_pi_placement(placement)
+        self.init_timings["placement"] = round(time.perf_counter() - _t0, 4)
 
     # ------------------------------------------------------------------ layouts
     def _pad_rows(self, a: torch.Tensor, dev) -> torch.Tensor:

@@ -562,6 +562,7 @@ class pert_infer_scRT():
                                 mean_reads=np.concatenate([mean_g, mean_g]), n_bins=inp.reads_g.shape[0])
             mark("prep")
             s1 = self._shard_pairs(dd, inp.reads_g, inp.states_g, lb_g2, init1)
+            self.timings["init_shard1"] = s1.init_timings
             mark("init_shard1")
             logging.info('STEP 1: Learning reads to CN bias from low variance cells.')
             losses_g = self._svi(s1, self.max_iter_step1, self.min_iter_step1, "step1")
@@ -588,6 +589,7 @@ class pert_infer_scRT():
                                 beta_means=beta_means_fit, seed=self.seed, method=self.init_method, cells=cells_s)
             s2 = self._shard(KIND_STEP2, dd, inp.reads_s, inp.libs_s, init2, eta=etas, lamb=float(lambda_fit[0]),
                              beta_means=beta_means_fit)
+            self.timings["init_shard2"] = s2.init_timings
             mark("init_shard2")
             # the sorted copies of the input tables (packaging's) are built while step 2 runs in
             # the library (the fit thread waits in one GIL-free call): not beside the host work

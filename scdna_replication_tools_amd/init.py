@@ -20,8 +20,12 @@ from scipy import special, stats
 
 
 def _median15(rng: np.random.Generator, ppf, shape):
+    """The median of 15 draws of the distribution with quantile function ``ppf``: the median
+    of an odd number of values is one of them and a quantile function is non-decreasing, so
+    median(ppf(u)) = ppf(median(u)) -- one ppf per site instead of 15 (the same values: the
+    beta / gamma / normal quantiles over 4 x 200 k draws, bit for bit)."""
     u = rng.uniform(1e-12, 1 - 1e-12, size=(15,) + tuple(shape))
-    return np.median(ppf(u), axis=0)
+    return ppf(np.median(u, axis=0))
 
 
 def init_params(kind: int, reads: Optional[np.ndarray], libs: np.ndarray, n_libs: int, P: int, K: int, *,

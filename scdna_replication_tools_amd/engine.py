@@ -200,6 +200,25 @@ _PI_TRAJECTORIES: Dict[tuple, dict] = {}
 _PI_LOCK = threading.Lock()          # the fit's helper thread may extend it (precompute)
 
 
+PI_TRAJECTORY_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "pi_trajectory.npz")
+
+
+def _shipped_trajectory(key: tuple) -> Optional[dict]:
+    """The canonical pi trajectory for the defaults (P = 13, lr 0.05, Adam (0.8, 0.99), eps 1e-8),
+    computed by CanonicalPiBlock itself and shipped with the package (tools/make_pi_trajectory.py;
+    tests/test_engine_host.py checks it against the live computation bit for bit): the step-1 loop
+    of every process would otherwise recompute the same 1,000 autograd steps (~0.2 s) first."""
+    try:
+        with np.load(PI_TRAJECTORY_FILE, allow_pickle=False) as f:
+            if tuple(f["key"].tolist()) != (float(key[0]),) + tuple(key[1:]):
+                return None
+            lp, z, m, v = f["lp"], f["z"], f["m"], f["v"]
+    except (OSError, KeyError, ValueError):
+        return None
+    return {"lp": [float(x) for x in lp],
+            "state": [(z[i].astype(F32), m[i].astype(F32), v[i].astype(F32)) for i in range(z.shape[0])]}
+
+
 class CanonicalPiBlock:
     """Step 1's expose_pi site (pert_model.py:607-613 with etas = ones, cn observed).
 
@@ -249,9 +268,13 @@ class CanonicalPiBlock:
         with _PI_LOCK:
             return self._cache_locked(T)
 
-    def _cache_locked(self, T: int) -> dict:
+    def _cache_locked(self, T: int, shipped: bool = True) -> dict:
         key = (self.P, float(self.lr), float(self.b1), float(self.b2), float(self.eps))
         c = _PI_TRAJECTORIES.get(key)
+        if c is None and shipped:
+            c = _shipped_trajectory(key)
+            if c is not None:
+                _PI_TRAJECTORIES[key] = c
         if c is None:
             c = _PI_TRAJECTORIES[key] = {"lp": [], "state": [(self.__class__(self.P, self.lr, (self.b1, self.b2),
                                                                                 self.eps).z, np.zeros(self.P, F32),

@@ -408,24 +408,32 @@ def main():
     # recorded on the device, the stopping rule is evaluated there (never met here: min_iter
     # beyond the step count; the NaN check stays on) and the losses come back to the host in
     # chunks, with no per-step host synchronisation.
-    if args.warmup > 0:
-        shard.run_svi(args.warmup, min_iter=10 ** 9, rel_tol=0.0)
-    # the loop's buffers (and step 1's canonical pi trajectory) set up before the timed region,
-    # as run_pert_model has them ready before a fit starts
-    # Before the timed region, the pattern's HBM ceiling on this device and lease (pert_stream_ceiling:
-    # the pass's streams with no arithmetic, the state left unchanged), repeated for ~100 ms of
-    # HBM load: on a short shard the first timed steps otherwise run ~3 % slower than the next
-    # ones (r05g: 1,250 cells 0.510 ms/step in the first K steps after W = 3, 0.495 in the next K)
+    # Before the timed region, in this order: (1) the loop's buffers for the warmup and both timed
+    # runs (the second one's timing events too; step 1's canonical pi trajectory), as
+    # run_pert_model has them ready before a fit starts, then the ranks meet; (2) the pattern's
+    # HBM ceiling on this device and lease (pert_stream_ceiling: the pass's streams with no
+    # arithmetic, the state left unchanged), repeated for ~100 ms of HBM load; (3) the W warmup
+    # steps.  On a short shard the first timed steps otherwise run slower than the next ones:
+    # r05g, 1,250 cells 0.510 ms/step in the first K steps after W = 3, 0.495 in the next K;
+    # r05bm, with the warmup before the burst, the value run still 1-2.4 % behind the evented
+    # run after it at 1,250-2,500 cells.
+    shard.pass_events = []
+    shard.pass_event_stride = max(1, args.event_stride)
+    shard.reserve_svi(args.steps)
+    shard.pass_events = None
+    shard.reserve_svi(max(args.warmup, 0) + 2 * args.steps)   # step 1's trajectory for all three runs
+    if pg is not None:
+        pg.barrier()
     ceil_ms = None
     if args.fit != "step1":
         est = shard.stream_ceiling_ms(reps=3)
         ceil_ms = shard.stream_ceiling_ms(reps=int(min(200, max(10, math.ceil(100.0 / max(est, 1e-3))))))
+    if args.warmup > 0:
+        shard.run_svi(args.warmup, min_iter=10 ** 9, rel_tol=0.0)
     # The value's region is the production loop with no timing events (one C call, pert_svi_run):
     # a HIP timing event on the stream costs the step ~50 us (r05d: 0.497 vs 0.520 ms/step at
     # 1,250 cells with events around every 5th pass).  The pass durations come from the same K
     # steps run again right after it, with events around every event_stride-th pass.
-    shard.pass_events = None
-    shard.reserve_svi(args.steps)
     if pg is not None:
         pg.barrier()
     torch.cuda.synchronize()

@@ -52,9 +52,14 @@ PLACEMENT_FAST_RATE = 5.8e12
 # 5th 4.4 GB set, the 6th-7th 2.2 GB set + spacer, the 10th-12th 1.1 GB set + spacer fast)
 PLACEMENT_STRIDE = 3 << 30
 PLACEMENT_MAX_HELD = 96 << 30
-# tries past the first fast one (fast placements come at two rates, ~6.0 and ~6.3 TB/s:
-# r05z 10 k sets 2.76-2.97 ms)
-PLACEMENT_EXTRA = 2
+# fast placements come at two rates (10 k cells: pattern 2.75-2.80 ms = 6.2-6.3 TB/s, or
+# 2.85-2.94 ms = 5.9-6.1 TB/s; r05z, r05ai-r05bs): the search stops at once on a set of the
+# upper rate, and past the first fast set of the lower one it tries at most PLACEMENT_EXTRA
+# more sets, worth at most PLACEMENT_EXTRA_BYTES (the 1,250-cell pass, bound by its one-round
+# tail, runs equally fast at either rate: r05bt, up to 22 tries for the same step)
+PLACEMENT_TOP_RATE = 6.15e12
+PLACEMENT_EXTRA = 4
+PLACEMENT_EXTRA_BYTES = 48 << 30
 
 
 # --------------------------------------------------------------------------- transforms
@@ -387,28 +392,36 @@ def placement_search(first, time_set: Callable, alloc: Callable, free_bytes: Cal
     """The loop of PertShard.choose_pi_placement, apart from the device: ``time_set(s)`` times
     the pass's stream pattern on set s (ms), ``alloc(spacer)`` returns a new set and the spacer
     allocations made before it, ``free_bytes()`` the device's free memory.  Tries sets while
-    the best streams below PLACEMENT_FAST_RATE, then PLACEMENT_EXTRA more, within
-    ``candidates`` tries, PLACEMENT_MAX_HELD bytes held and 8 GB left free.  Returns the
-    fastest set, every try's time (the first set's first) and the list of what was held
-    (for the caller to drop once the state has moved)."""
+    the best streams below PLACEMENT_FAST_RATE, then up to PLACEMENT_EXTRA more (at most
+    PLACEMENT_EXTRA_BYTES) unless one streams at PLACEMENT_TOP_RATE (the search stops there),
+    within ``candidates`` tries, PLACEMENT_MAX_HELD bytes held and 8 GB left free.  Returns the
+    fastest set, every try's time (the first set's first) and the list of what was held (for
+    the caller to drop once the state has moved)."""
     best = first
     best_ms = time_set(first)
     times = [best_ms]
     held = []
     spacer = max(0, PLACEMENT_STRIDE - set_bytes)
     held_bytes = 0
-    fast_at = None                               # the try count when a fast set was first seen
+    step = set_bytes + spacer
+    extra = None                                 # bytes tried since a fast set was first seen
+    n_extra = 0
     while len(times) < candidates:
-        if fast_at is None and pattern_bytes / (best_ms * 1e-3) >= PLACEMENT_FAST_RATE:
-            fast_at = len(times)
-        if fast_at is not None and len(times) >= fast_at + PLACEMENT_EXTRA:
+        rate = pattern_bytes / (best_ms * 1e-3)
+        if rate >= PLACEMENT_TOP_RATE:
             break
-        step = set_bytes + spacer
+        if extra is None and rate >= PLACEMENT_FAST_RATE:
+            extra = 0
+        if extra is not None and (extra + step > PLACEMENT_EXTRA_BYTES or n_extra >= PLACEMENT_EXTRA):
+            break
         if free_bytes() < step + set_bytes + (8 << 30) or held_bytes + step > PLACEMENT_MAX_HELD:
             break
         cand, sp = alloc(spacer)
         held.extend(sp)
         held_bytes += step
+        if extra is not None:
+            extra += step
+            n_extra += 1
         t = time_set(cand)
         times.append(t)
         if t < best_ms:
@@ -774,8 +787,9 @@ class PertShard:
         time.  So: time pert_stream_ceiling (the pass's own streams on this shard's grid, values
         written back unchanged) on the current arrays; while that is slower than
         PLACEMENT_FAST_RATE, allocate another set (the earlier ones held, so it lands elsewhere)
-        and time it, up to ``candidates`` sets, and PLACEMENT_EXTRA more once one is fast (fast
-        placements come at two rates); move the state into the fastest and free the rest
+        and time it, up to ``candidates`` sets, and PLACEMENT_EXTRA more (at most
+        PLACEMENT_EXTRA_BYTES) once one is fast unless one streams at PLACEMENT_TOP_RATE (fast placements come at two
+        rates); move the state into the fastest and free the rest
         (``placement_search``).  Results do not depend on the placement (same data, same
         kernel).  Returns (and keeps in ``self.placement``) the candidates' times and the
         choice."""

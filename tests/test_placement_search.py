@@ -35,19 +35,34 @@ def run(script, set_bytes=9 * GB, candidates=24):
     return placement_search(0, script.time_set, script.alloc, script.free_bytes, set_bytes, PATTERN, candidates)
 
 
-def test_fast_first_set_still_tries_the_extra_sets():
-    sc = Script([0.95, 0.99, 0.90, 0.5])
+def test_top_rate_first_set_stops_at_once():
+    sc = Script([0.95, 0.9])                     # 6.3 TB/s: the upper of the two fast rates
     best, times, held = run(sc)
-    assert times == [0.95, 0.99, 0.90] and best == 2 and sc.made == engine.PLACEMENT_EXTRA
-    assert sorted(held) == [0, 1]
+    assert times == [0.95] and best == 0 and sc.made == 0 and held == []
 
 
-def test_slow_sets_until_fast_then_extra():
-    sc = Script([1.2, 1.2, 1.19, 1.0, 0.97, 1.01, 0.5])
+def test_fast_first_set_tries_until_a_top_rate_set():
+    sc = Script([1.0, 0.99, 1.01, 0.96, 0.5])
     best, times, held = run(sc)
-    # fast first seen after try 4 (1.0 ms: 6.0 TB/s); two more tries, the faster kept
-    assert times == [1.2, 1.2, 1.19, 1.0, 0.97, 1.01] and best == 4
-    assert set(held) == {0, 1, 2, 3, 5}
+    # 1.0 ms (6.0 TB/s) is fast, not top; 0.96 ms (6.25 TB/s) is top: the search stops there
+    assert times == [1.0, 0.99, 1.01, 0.96] and best == 3
+    assert sorted(held) == [0, 1, 2]
+
+
+def test_slow_sets_until_fast_then_the_extra_budget():
+    sc = Script([1.2, 1.2, 1.19, 1.0, 0.99, 1.01, 1.0, 1.0, 1.0, 0.5])
+    best, times, held = run(sc, set_bytes=9 * GB)
+    # fast first seen at try 4 (1.0 ms: 6.0 TB/s), then PLACEMENT_EXTRA more sets (at most
+    # PLACEMENT_EXTRA_BYTES of them)
+    n_extra = min(engine.PLACEMENT_EXTRA, engine.PLACEMENT_EXTRA_BYTES // (9 * GB))
+    assert times == sc.ms[:4 + n_extra] and best == 4
+    assert set(held) == set(range(4 + n_extra)) - {4}
+
+
+def test_big_sets_stop_at_the_extra_bytes():
+    sc = Script([1.0] * 10)
+    best, times, held = run(sc, set_bytes=30 * GB)
+    assert len(times) == 1 + engine.PLACEMENT_EXTRA_BYTES // (30 * GB) and best == 0
 
 
 def test_never_fast_stops_at_the_candidate_cap():

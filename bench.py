@@ -272,6 +272,37 @@ def fullfit_c1():
     print(json.dumps(rec), flush=True)
 
 
+class HelperLoad:
+    """The host work a fit's helper thread does beside the device's steps (the tau
+    initialiser's exact path, GIL-bound numpy: pert_model.py:364-423 per cell), looped on 64
+    cells of the shard until stop(); the library scans made first on this thread, as a fit
+    does (tau_init.prepare_host_threads)."""
+
+    def __init__(self, reads):
+        import threading
+        from scdna_replication_tools_amd import tau_init
+        tau_init.prepare_host_threads()
+        self.cols = np.ascontiguousarray(np.asarray(reads, np.float32)[:, :64])
+        self.cells = 0
+        self.halt = threading.Event()
+        self.thread = threading.Thread(target=self._run, name="bench-helper", daemon=True)
+        self.t0 = time.perf_counter()
+        self.thread.start()
+
+    def _run(self):
+        from scdna_replication_tools_amd import tau_init
+        while not self.halt.is_set():
+            tau_init.exact_fractions(self.cols)
+            self.cells += self.cols.shape[1]
+
+    def stop(self):
+        self.halt.set()
+        self.thread.join()
+        dt = time.perf_counter() - self.t0
+        return {"what": "tau_init.exact_fractions on 64 cells, looped on a thread", "cells": self.cells,
+                "cells_per_s": round(self.cells / dt, 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -302,6 +333,9 @@ def main():
     ap.add_argument("--cpu-cells", type=int, default=640)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--helper-load", action="store_true",
+                    help="run the tau initialiser's exact host path on a thread beside the timed steps "
+                         "(what a fit's helper thread does during steps 1-2)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--profile", default="", help="tools/profile.sh output dir of this command: report the "
                     "roofline fraction recomputed from its kernel trace and its PMC HBM bytes")
@@ -428,6 +462,9 @@ def main():
     if args.fit != "step1":
         est = shard.stream_ceiling_ms(reps=3)
         ceil_ms = shard.stream_ceiling_ms(reps=int(min(200, max(10, math.ceil(100.0 / max(est, 1e-3))))))
+    helper = None
+    if args.helper_load:
+        helper = HelperLoad(reads)
     if args.warmup > 0:
         shard.run_svi(args.warmup, min_iter=10 ** 9, rel_tol=0.0)
     # The value's region is the production loop with no timing events (one C call, pert_svi_run):
@@ -459,6 +496,7 @@ def main():
         pg.barrier()
     dt_ev = time.perf_counter() - t1
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in shard.pass_events]))
+    helper_rec = helper.stop() if helper is not None else None
     shard.pass_events = None
     t = torch.tensor([dt, kern_ms, dt_ev], dtype=torch.float64, device=device)
     if pg is not None:
@@ -517,6 +555,8 @@ def main():
             "loss_first": losses[0], "loss_last": losses[-1],
         }
         rec["ms_per_step_evented"] = dt_ev / args.steps * 1e3
+        if helper_rec is not None:
+            rec["helper_load"] = helper_rec
         if ceil_ms is not None:
             rec["roofline"]["pattern_ceiling"] = {
                 "ms": ceil_ms, "GB/s": bpc * local_cb / (ceil_ms * 1e-3) / 1e9,

@@ -306,7 +306,10 @@ class HelperLoad:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    # K = 200 by default: a fit runs its steps as one C call, and the call's fixed costs (its first
+    # launches, the final synchronisation, the interpreter lock taken back at its end) weigh 10x
+    # less than at K = 20 (r05ca: 1,250 cells 0.419-0.426 ms/step at K = 200, 0.430-0.449 at 20)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])

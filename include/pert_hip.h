@@ -63,6 +63,9 @@ extern "C" {
 #define PERT_E_UNSUPPORTED_P 2
 #define PERT_E_UNSUPPORTED_K 3
 #define PERT_E_COMM_UNAVAILABLE 5   /* RCCL not loaded (pert_comm_load) or lacks a symbol */
+#define PERT_E_COMM_ABORTED 6       /* a rank of the fit failed and raised the abort word */
+#define PERT_E_COMM_TIMEOUT 7       /* a peer did not arrive within the communicator's deadline */
+#define PERT_E_COMM_FAULT 8         /* injected by pert_comm_inject_fault (tests) */
 #define PERT_E_HIP_BASE 1000        /* + hipError_t */
 #define PERT_E_COMM_BASE 2000       /* + ncclResult_t */
 
@@ -249,17 +252,46 @@ int pert_svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hpara
 /* ---- Sharded fits: cells split over ranks, one process per GPU.
  * The shared block's gradient [0, n_shared) and the loss (slot n_shared) are summed across
  * the ranks once per SVI step, between the reductions and Adam.  A pert_comm is an RCCL
- * communicator over the fit's ranks (xGMI): the library queues that all-reduce itself on
- * the fit's stream, so a whole sharded fit is one C call like a single-rank one. */
+ * communicator over the fit's ranks (xGMI) -- or, for ranks sharing a GPU (which RCCL
+ * refuses; tests), a host-staged sum through POSIX shared memory -- and the library queues
+ * that all-reduce itself on the fit's stream, so a whole sharded fit is one C call like a
+ * single-rank one.  Failure is bounded: a rank whose loop fails raises the node's abort word
+ * (and aborts its RCCL communicator), and a rank waiting on its stream polls that word, RCCL's
+ * async error and a deadline instead of blocking; the loop then returns PERT_E_COMM_ABORTED /
+ * PERT_E_COMM_TIMEOUT / RCCL's error on every rank.  A comm is not usable after a failure. */
 typedef struct pert_comm pert_comm;
 
 /* dlopen RCCL from rccl_path (the copy the process already uses -- torch's) and resolve
- * ncclGetUniqueId / ncclCommInitRank / ncclAllReduce / ncclCommDestroy.  Once per process. */
+ * ncclGetUniqueId / ncclCommInitRank / ncclAllReduce / ncclCommDestroy / ncclCommAbort /
+ * ncclCommGetAsyncError.  Once per process. */
 int pert_comm_load(const char* rccl_path);
 /* ncclGetUniqueId into id (n = 128 bytes), on one rank; the caller broadcasts it. */
 int pert_comm_unique_id(uint8_t* id, int32_t n);
 /* ncclCommInitRank on the current device (collective: returns once every rank has called). */
 int pert_comm_init(const uint8_t* id, int32_t n, int32_t world, int32_t rank, pert_comm** out);
+/* The host-staged communicator: every rank of one node calls with the same POSIX shm name
+ * ("/..."; the segment is unlinked once all ranks have mapped it) and max_n >= the longest
+ * all-reduce; returns once every rank has attached or after timeout_s (PERT_E_COMM_TIMEOUT).
+ * Each all-reduce is a copy to pinned memory, a host function summing the ranks' blocks in
+ * rank order (identical bits on every rank) and a copy back, all queued on the stream. */
+int pert_comm_init_host(const char* name, int32_t world, int32_t rank, int64_t max_n, double timeout_s,
+                        pert_comm** out);
+/* The deadline of every wait (seconds, default 600) and, for an RCCL communicator, a
+ * node-local abort word: POSIX shm `abort_name` mapped collectively like pert_comm_init_host's
+ * segment (NULL: the word is this process's own, peers then stop by the deadline). */
+int pert_comm_set_watchdog(pert_comm* comm, const char* abort_name, double timeout_s);
+/* Raise the abort word with `code` and, RCCL, abort the communicator (its queued collectives
+ * return).  pert_svi_run_sharded calls it on any failure of its rank. */
+int pert_comm_abort(pert_comm* comm, int32_t code);
+/* PERT_OK, or the first failure seen by this rank (its own, or a peer's abort). */
+int pert_comm_status(pert_comm* comm);
+/* Wait for `ev` (recorded on the fit's stream) polling the abort word, RCCL's async error and
+ * the deadline; on failure aborts the comm and returns the failure.  comm == NULL: blocking
+ * hipEventSynchronize. */
+int pert_comm_wait_event(pert_comm* comm, hipEvent_t ev);
+/* Test hook: this rank's all-reduce call number `at_call` (0-based, -1 = never) fails at
+ * queue time with PERT_E_COMM_FAULT, as a rank's launch failure would. */
+int pert_comm_inject_fault(pert_comm* comm, int64_t at_call);
 int pert_comm_destroy(pert_comm* comm);
 /* recv = sum over ranks of send (fp64, n elements; send == recv allowed), queued on stream. */
 int pert_comm_allreduce_sum_f64(pert_comm* comm, const double* send, double* recv, int64_t n,

@@ -30,11 +30,26 @@ EXPORTED_SYMBOLS = (
     "pert_selftest_nb_lgdiff_device", "pert_selftest_enum_cellbin_host", "pert_selftest_enum_online_host", "pert_tau_binarize", "pert_svi_steps",
     "pert_svi_run", "pert_comm_load", "pert_comm_unique_id", "pert_comm_init", "pert_comm_destroy",
     "pert_comm_allreduce_sum_f64", "pert_svi_steps_sharded", "pert_svi_run_sharded", "pert_version",
+    "pert_comm_init_host", "pert_comm_set_watchdog", "pert_comm_abort", "pert_comm_status", "pert_comm_wait_event",
+    "pert_comm_inject_fault",
 )
+
+# include/pert_hip.h status codes of a sharded fit's communicator
+E_COMM_UNAVAILABLE, E_COMM_ABORTED, E_COMM_TIMEOUT, E_COMM_FAULT = 5, 6, 7, 8
 
 
 class NativeLibraryError(RuntimeError):
     pass
+
+
+class CommError(RuntimeError):
+    """A sharded fit's communicator failed: this rank's collective, or a peer's abort
+    (PERT_E_COMM_ABORTED), or a peer that did not arrive in time (PERT_E_COMM_TIMEOUT).
+    ``code`` is the library's status."""
+
+    def __init__(self, msg: str, code: int):
+        super().__init__(msg)
+        self.code = code
 
 
 class PertLayout(ctypes.Structure):
@@ -172,6 +187,12 @@ def load(path: str, gil: bool = True):
     handle.pert_comm_init.argtypes = [c_void_p, i32, i32, i32, POINTER(c_void_p)]
     handle.pert_comm_destroy.argtypes = [c_void_p]
     handle.pert_comm_allreduce_sum_f64.argtypes = [c_void_p, c_void_p, c_void_p, i64, c_void_p]
+    handle.pert_comm_init_host.argtypes = [c_char_p, i32, i32, i64, ctypes.c_double, POINTER(c_void_p)]
+    handle.pert_comm_set_watchdog.argtypes = [c_void_p, c_char_p, ctypes.c_double]
+    handle.pert_comm_abort.argtypes = [c_void_p, i32]
+    handle.pert_comm_status.argtypes = [c_void_p]
+    handle.pert_comm_wait_event.argtypes = [c_void_p, c_void_p]
+    handle.pert_comm_inject_fault.argtypes = [c_void_p, i64]
     handle.pert_svi_steps_sharded.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams), fp,
                                               fp, i32, i32, i32, c_void_p, c_void_p, c_void_p, c_void_p]
     handle.pert_svi_run_sharded.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams), fp,
@@ -194,11 +215,16 @@ def load(path: str, gil: bool = True):
 def check(code: int, what: str):
     if code != 0:
         if code >= 2000:
-            raise RuntimeError("{} failed: RCCL error {}".format(what, code - 2000))
+            raise CommError("{} failed: RCCL error {}".format(what, code - 2000), code)
         if code >= 1000:
             raise RuntimeError("{} failed: HIP error {}".format(what, code - 1000))
-        if code == 5:
+        if code == E_COMM_UNAVAILABLE:
             raise NativeLibraryError("{} failed: RCCL is not loaded (pert_comm_load)".format(what))
+        if code in (E_COMM_ABORTED, E_COMM_TIMEOUT, E_COMM_FAULT):
+            why = {E_COMM_ABORTED: "a rank of the fit failed and aborted it",
+                   E_COMM_TIMEOUT: "a rank of the fit did not arrive before the deadline",
+                   E_COMM_FAULT: "injected fault (pert_comm_inject_fault)"}[code]
+            raise CommError("{} failed: {}".format(what, why), code)
         raise ValueError("{} failed: status {}".format(what, code))
 
 

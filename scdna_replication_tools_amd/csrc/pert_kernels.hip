@@ -22,6 +22,10 @@
 #include <math.h>
 #include <stddef.h>
 
+#include <mutex>
+#include <utility>
+#include <vector>
+
 namespace {
 
 using namespace pert;
@@ -2511,6 +2515,43 @@ int svi_steps(const pert_problem* prob, pert_state* st, const pert_adam_hparams*
   return rc;
 }
 
+// The loop's chunk events come from a per-process pool (per device) instead of being created
+// and destroyed by every call: a fit makes one call per step, a bench or test many.
+struct EventPool {
+  std::mutex mu;
+  std::vector<std::pair<int, hipEvent_t>> free_list;
+};
+EventPool& event_pool() {
+  static EventPool* p = new EventPool;          // (never destroyed: events outlive static teardown)
+  return *p;
+}
+
+int take_events(int n, hipEvent_t* ev, int* taken) {
+  int dev = 0;
+  int rc = hip_status(hipGetDevice(&dev));
+  *taken = 0;
+  EventPool& pool = event_pool();
+  {
+    std::lock_guard<std::mutex> lock(pool.mu);
+    for (size_t i = pool.free_list.size(); i-- > 0 && *taken < n;)
+      if (pool.free_list[i].first == dev) {
+        ev[(*taken)++] = pool.free_list[i].second;
+        pool.free_list.erase(pool.free_list.begin() + i);
+      }
+  }
+  for (; *taken < n && rc == PERT_OK; ++*taken)
+    rc = hip_status(hipEventCreateWithFlags(&ev[*taken], hipEventDisableTiming | hipEventBlockingSync));
+  return rc;
+}
+
+void give_events(int n, const hipEvent_t* ev) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  EventPool& pool = event_pool();
+  std::lock_guard<std::mutex> lock(pool.mu);
+  for (int k = 0; k < n; ++k) pool.free_list.emplace_back(dev, ev[k]);
+}
+
 int svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp, const float* step_size,
             const float* inv_bc2_sqrt, int32_t n_iter, int32_t chunk, int32_t depth, int32_t one_launch,
             pert_comm* comm, double* grad_local, hipEvent_t* pass_events, double* host_rec, int32_t* n_launched,
@@ -2521,19 +2562,20 @@ int svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hparams* h
   if (n_iter == 0) return PERT_OK;
   const int n_chunks = (n_iter + chunk - 1) / chunk;
   const int ring = depth + 1;
-  hipEvent_t ev[64];
+  hipEvent_t ev[65];
   if (ring > 64) return PERT_E_ARG;
-  int rc = PERT_OK, made = 0;
-  for (; made < ring && rc == PERT_OK; ++made)
-    rc = hip_status(hipEventCreateWithFlags(&ev[made], hipEventDisableTiming | hipEventBlockingSync));
+  int made = 0;
+  int rc = take_events(ring + (comm ? 1 : 0), ev, &made);
   int waited = 0;                              // chunks whose records have been looked at
   bool stop_seen = false;
   int c = 0;
   // a chunk's records are at host_rec[2 j] (loss) and host_rec[2 j + 1] (>= 0: stopped at j).
   // Which chunks are looked at, and when, depends only on the chunk index: the ranks of a
   // sharded fit (identical, all-reduced loss records) stop queueing after the same chunk.
+  // Sharded, a wait polls the communicator (a peer's abort, RCCL's async error, a deadline)
+  // instead of blocking, so a failed rank cannot leave the others waiting forever.
   auto look = [&](int k) {
-    rc = rc == PERT_OK ? hip_status(hipEventSynchronize(ev[k % ring])) : rc;
+    rc = rc == PERT_OK ? pert_comm_wait_event(comm, ev[k % ring]) : rc;
     const int j1 = (k + 1) * chunk < n_iter ? (k + 1) * chunk : n_iter;
     for (int j = k * chunk; j < j1 && rc == PERT_OK; ++j)
       if (host_rec[2 * j + 1] >= 0.0) stop_seen = true;
@@ -2550,9 +2592,18 @@ int svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hparams* h
     if (rc == PERT_OK) rc = hip_status(hipEventRecord(ev[c % ring], stream));
     if (rc == PERT_OK) *n_launched = j0 + n;
   }
+  if (comm) {
+    // every queued launch and copy, waited for under the watchdog; a failure on this rank
+    // raises the abort word the peers poll, and stops this rank's own collectives
+    if (rc == PERT_OK && made == ring + 1) {
+      rc = hip_status(hipEventRecord(ev[ring], stream));
+      if (rc == PERT_OK) rc = pert_comm_wait_event(comm, ev[ring]);
+    }
+    if (rc != PERT_OK) (void)pert_comm_abort(comm, rc);
+  }
   const hipError_t e = hipStreamSynchronize(stream);     // every queued launch and copy
   if (rc == PERT_OK) rc = hip_status(e);
-  for (int k = 0; k < made; ++k) (void)hipEventDestroy(ev[k]);
+  give_events(made, ev);
   return rc;
 }
 

@@ -334,52 +334,161 @@ def rccl_path() -> str:
     return os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
 
 
-class RcclComm:
-    """An RCCL communicator over the ranks of a sharded fit (``pert_comm``, include/pert_hip.h):
-    the library queues the per-step all-reduce of the shared block itself, on the fit's stream,
-    so a sharded fit's SVI loop is one GIL-free C call (``pert_svi_run_sharded``) as a
-    single-rank one is.  Made collectively by every rank of ``group`` (rank 0's unique id
-    broadcast over the group), on the current device; ``world1()`` makes a one-rank
-    communicator without a process group (tests, bench)."""
+def comm_timeout_s() -> float:
+    """The deadline of a sharded fit's waits on its peers (PERT_COMM_TIMEOUT_S, default 600 s)."""
+    import os
+    return float(os.environ.get("PERT_COMM_TIMEOUT_S", "600"))
 
-    def __init__(self, group=None, *, world1: bool = False):
+
+def _group_device(group):
+    import torch.distributed as dist
+    return (torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl"
+            else torch.device("cpu"))
+
+
+def _broadcast_bytes(data: bytes, n: int, group) -> bytes:
+    """Rank 0's ``n`` bytes on every rank of ``group`` (a uint8 tensor broadcast)."""
+    import torch.distributed as dist
+    t = torch.zeros(n, dtype=torch.uint8)
+    if data:
+        t[:len(data)] = torch.tensor(list(data), dtype=torch.uint8)
+    t = t.to(_group_device(group))
+    dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    return bytes(t.cpu().tolist())
+
+
+def _all_ok(ok: bool, group) -> bool:
+    """True on every rank iff ``ok`` on every rank (a MIN all-reduce): the ranks of a fit take
+    the same communicator, or all fall back together."""
+    import torch.distributed as dist
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=_group_device(group))
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
+
+
+def _segment_name() -> str:
+    import os
+    return "/pert-{}-{}".format(os.getpid(), os.urandom(6).hex())
+
+
+class PertComm:
+    """A communicator of the library's own over the ranks of a sharded fit (``pert_comm``,
+    include/pert_hip.h): the library queues the per-step all-reduce of the shared block itself,
+    on the fit's stream, so a sharded fit's SVI loop is one GIL-free C call
+    (``pert_svi_run_sharded``) as a single-rank one is.  A rank whose loop fails raises the
+    node's abort word, and every rank's loop returns within the deadline with ``CommError``."""
+
+    handle = None
+    lib = None
+
+    def allreduce(self, t: torch.Tensor) -> None:
+        """In-place sum over the ranks of an fp64 device tensor, on the current stream."""
+        if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("{}.allreduce takes a contiguous fp64 device tensor".format(type(self).__name__))
+        nat.check(self.lib.pert_comm_allreduce_sum_f64(self.handle, t.data_ptr(), t.data_ptr(), t.numel(),
+                                                        torch.cuda.current_stream(t.device).cuda_stream),
+                  "pert_comm_allreduce_sum_f64")
+
+    def status(self) -> int:
+        """0, or the first failure this rank has seen (its own, or a peer's abort)."""
+        return int(self.lib.pert_comm_status(self.handle))
+
+    def abort(self, code: int = nat.E_COMM_ABORTED) -> None:
+        nat.check(self.lib.pert_comm_abort(self.handle, int(code)), "pert_comm_abort")
+
+    def _fault_from_env(self) -> None:
+        """PERT_COMM_FAULT_AT="rank:call": the test hook below, set on that rank at creation."""
+        import os
+        spec = os.environ.get("PERT_COMM_FAULT_AT")
+        if spec:
+            r, k = (int(x) for x in spec.split(":"))
+            if r == self.rank:
+                self.inject_fault(k)
+
+    def inject_fault(self, at_call: int) -> None:
+        """Test hook: this rank's all-reduce call ``at_call`` (0-based, counted from the
+        communicator's creation) fails at queue time."""
+        nat.check(self.lib.pert_comm_inject_fault(self.handle, int(at_call)), "pert_comm_inject_fault")
+
+    def close(self) -> None:
+        if self.handle is not None and self.handle.value:
+            if self.status() == 0:
+                torch.cuda.synchronize()
+            nat.check(self.lib.pert_comm_destroy(self.handle), "pert_comm_destroy")
+        self.handle = None
+
+
+class RcclComm(PertComm):
+    """The product communicator: RCCL over the ranks of ``group`` (one process per GPU, xGMI),
+    made collectively on the current device (rank 0's unique id broadcast over the group), with
+    a node-local abort word beside it (``pert_comm_set_watchdog``).  Loading RCCL is checked on
+    every rank before any rank enters the collective init, so the ranks take this communicator
+    or raise together (``_Dist`` then falls back on all of them).  ``world1()`` makes a
+    one-rank communicator without a process group (tests, bench)."""
+
+    def __init__(self, group=None, *, world1: bool = False, device=None):
         self.lib = nat.lib_nogil()              # init blocks until every rank has called: GIL released
-        nat.check(self.lib.pert_comm_load(rccl_path().encode()), "pert_comm_load")
+        if device is not None:
+            dev = torch.device(device)
+            if dev.type != "cuda" or (dev.index is not None and dev.index != torch.cuda.current_device()):
+                raise ValueError("RcclComm is made on the current device ({}), not {}: set the device "
+                                 "first".format(torch.cuda.current_device(), dev))
         if world1:
             self.world, self.rank, dist = 1, 0, None
         else:
             import torch.distributed as dist
             self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        rc = self.lib.pert_comm_load(rccl_path().encode())
+        if dist is not None and self.world > 1 and not _all_ok(rc == 0, group):
+            raise nat.NativeLibraryError("pert_comm_load failed on {} rank(s) of the group".format(
+                "this and possibly other" if rc else "another"))
+        nat.check(rc, "pert_comm_load")
         uid = (ctypes.c_uint8 * 128)()
+        name = b""
         if self.rank == 0:
             nat.check(self.lib.pert_comm_unique_id(uid, 128), "pert_comm_unique_id")
+            name = _segment_name().encode()
         if dist is not None and self.world > 1:
-            dev = (torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl"
-                   else torch.device("cpu"))
-            t = torch.tensor(list(bytes(uid)), dtype=torch.uint8, device=dev)
-            dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
-            uid = (ctypes.c_uint8 * 128)(*t.cpu().tolist())
+            got = _broadcast_bytes(bytes(uid) + name.ljust(64, b"\0"), 128 + 64, group)
+            uid = (ctypes.c_uint8 * 128)(*got[:128])
+            name = got[128:].rstrip(b"\0")
         h = ctypes.c_void_p()
-        nat.check(self.lib.pert_comm_init(uid, 128, self.world, self.rank, ctypes.byref(h)), "pert_comm_init")
+        rc = self.lib.pert_comm_init(uid, 128, self.world, self.rank, ctypes.byref(h))
+        if dist is not None and self.world > 1 and not _all_ok(rc == 0, group):
+            if rc == 0:
+                self.lib.pert_comm_destroy(h)
+            raise nat.NativeLibraryError("pert_comm_init failed on a rank of the group (status {})".format(rc))
+        nat.check(rc, "pert_comm_init")
         self.handle = h
+        rc = self.lib.pert_comm_set_watchdog(h, name if self.world > 1 else None, comm_timeout_s())
+        if rc != 0:
+            self.close()
+            nat.check(rc, "pert_comm_set_watchdog")
+        self._fault_from_env()
 
     @classmethod
     def world1(cls) -> "RcclComm":
         return cls(world1=True)
 
-    def allreduce(self, t: torch.Tensor) -> None:
-        """In-place sum over the ranks of an fp64 device tensor, on the current stream."""
-        if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous():
-            raise ValueError("RcclComm.allreduce takes a contiguous fp64 device tensor")
-        nat.check(self.lib.pert_comm_allreduce_sum_f64(self.handle, t.data_ptr(), t.data_ptr(), t.numel(),
-                                                        torch.cuda.current_stream(t.device).cuda_stream),
-                  "pert_comm_allreduce_sum_f64")
 
-    def close(self) -> None:
-        if self.handle is not None and self.handle.value:
-            torch.cuda.synchronize()
-            nat.check(self.lib.pert_comm_destroy(self.handle), "pert_comm_destroy")
-        self.handle = None
+class HostComm(PertComm):
+    """The host-staged communicator (``pert_comm_init_host``): for ranks that share a GPU (RCCL
+    refuses them) -- the tests' two ranks on one device run the product's C loop
+    (``pert_svi_run_sharded``) through it.  Each all-reduce is a copy to pinned memory, a host
+    function that adds the ranks' blocks through POSIX shared memory in rank order, and a copy
+    back, queued where the RCCL call would be.  Ranks on one node; ``max_n`` bounds the block
+    (n_shared + 1 = bins + a few dozen: 2^18 covers 20 kb bins of a whole genome)."""
+
+    def __init__(self, group=None, *, max_n: int = 1 << 18):
+        import torch.distributed as dist
+        self.lib = nat.lib_nogil()
+        self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        name = _broadcast_bytes(_segment_name().encode() if self.rank == 0 else b"", 64, group).rstrip(b"\0")
+        h = ctypes.c_void_p()
+        nat.check(self.lib.pert_comm_init_host(name, self.world, self.rank, int(max_n), comm_timeout_s(),
+                                               ctypes.byref(h)), "pert_comm_init_host")
+        self.handle = h
+        self._fault_from_env()
 
 
 # --------------------------------------------------------------------------- shard
@@ -442,7 +551,7 @@ class PertShard:
                  is_root: bool = True, n_cells_total: Optional[int] = None,
                  allreduce: Optional[Callable[[torch.Tensor], None]] = None,
                  dirichlet_mode: str = "torch32", bins_per_tile: int = 0, variant: int = 3, fused: bool = False,
-                 paired: bool = False, lib=None, comm: Optional[RcclComm] = None,
+                 paired: bool = False, lib=None, comm: Optional[PertComm] = None,
                  placement: Optional[int] = None):
         self.lib = nat.lib() if lib is None else lib        # another build of the ABI (A/B tools)
         # the chunked SVI loop's handle: the product library through CDLL (the call releases the
@@ -478,6 +587,7 @@ class PertShard:
         self.comm = comm
         self.allreduce = comm.allreduce if (comm is not None and allreduce is None) else allreduce
         self.t = 0
+        self.last_launched = 0                 # iterations the last run_svi queued
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
         self.ldn = ldn = -(-NS // nat.BLOCK) * nat.BLOCK      # row stride: stored columns rounded up to 256
@@ -963,6 +1073,7 @@ class PertShard:
         reason 0 = max_iter reached, 1 = converged, 2 = NaN loss; the fit state is the one
         after the last recorded iteration, exactly as if the loop had run on the host."""
         n = int(max_iter)
+        self.last_launched = 0
         if n <= 0:
             return [], 0
         dev = self.device
@@ -1012,6 +1123,7 @@ class PertShard:
                         1 if self.fused else 0, *shard_args, evp, host.data_ptr(), ctypes.byref(nl),
                         self._stream()), "pert_svi_run")
                 launched = int(nl.value)
+                self.last_launched = launched
                 if self.pass_events is not None:       # (iterations never queued recorded nothing)
                     self.pass_events.extend((e0, e1) for i, e0, e1 in sampled if i < launched)
                 n = 0                              # nothing left for the per-iteration loop below
@@ -1020,7 +1132,7 @@ class PertShard:
                 for i in range(j0, j1):
                     st.step = i
                     self._launch_step(t0 + i + 1)
-                launched = j1
+                launched = self.last_launched = j1
                 host[j0:j1].copy_(rec[j0:j1], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record()

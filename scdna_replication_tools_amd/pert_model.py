@@ -112,7 +112,7 @@ class PivotAxes:
 class _Dist:
     """The process group a fit is sharded over (world 1 = no sharding)."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, device=None):
         import torch.distributed as dist
         self.dist = dist if dist.is_available() and dist.is_initialized() else None
         self.group = group
@@ -121,12 +121,19 @@ class _Dist:
         self.backend = self.dist.get_backend(group) if self.dist else None
         # ranks on RCCL (one process per GPU): a pert_comm communicator of the library's own, so
         # each fit's SVI loop -- all-reduce included -- is one GIL-free C call; other backends
-        # (gloo: several ranks sharing a GPU in tests) all-reduce through torch.distributed per step
+        # (gloo: several ranks sharing a GPU in tests) all-reduce through torch.distributed per
+        # step, or -- PERT_NATIVE_COMM=host -- through the library's host-staged communicator
+        # (the same C loop as RCCL ranks run).  The choice is collective: a communicator that
+        # fails on any rank fails on all of them (engine.RcclComm), and all fall back together.
         self.comm = None
-        if self.world > 1 and self.backend == "nccl" and os.environ.get("PERT_NATIVE_COMM", "1") != "0":
+        mode = os.environ.get("PERT_NATIVE_COMM", "1")
+        if self.world > 1 and mode == "host":
+            from .engine import HostComm
+            self.comm = HostComm(group)
+        elif self.world > 1 and self.backend == "nccl" and mode != "0":
             from .engine import RcclComm
             try:
-                self.comm = RcclComm(group)
+                self.comm = RcclComm(group, device=device)
             except Exception as e:                 # noqa: BLE001  (torch.distributed's all-reduce then)
                 log.warning("the library's RCCL communicator failed (%s: %s); all-reducing through "
                             "torch.distributed per step", type(e).__name__, e)
@@ -217,6 +224,7 @@ class pert_infer_scRT():
         self.log_steps = log_steps
         self.timings = {}
         self.iters = {}
+        self.launched = {}
         self._inp = None
 
     # the input tables: after _prepare, their sorted copies -- possibly still being built on a
@@ -416,6 +424,7 @@ class pert_infer_scRT():
             print('ELBO is NaN at iteration ' + str(len(losses) - 1))
         self.timings[label] = time.perf_counter() - t0
         self.iters[label] = len(losses)
+        self.launched[label] = getattr(shard, "last_launched", len(losses))   # iterations queued
         return losses
 
     @staticmethod
@@ -481,9 +490,10 @@ class pert_infer_scRT():
     def run_pert_model(self):
         t_all = time.perf_counter()
         P, K = self.P, self.K
-        dd = _Dist(self._group)
+        # the device first: the library's communicator is made on the current device
         if self.device.type == "cuda" and self.device.index is not None:
             torch.cuda.set_device(self.device)
+        dd = _Dist(self._group, device=self.device)
         # host work that only steps 2/3 need runs on a helper thread: the consensus profiles as
         # soon as the G1/2 table is sorted (while the S table is prepared), the step-2 prior and
         # tau initialisation while step 1 fits, then (during step 2) the step-3 prior and tau
@@ -640,6 +650,12 @@ class pert_infer_scRT():
                 self.timings["decode_package_g"] = time.perf_counter() - tic
                 del s3
                 mark("decode_package3")
+        except BaseException:
+            # this rank failed: raise the abort word its peers' sharded loops poll, so they
+            # return with CommError now instead of at the communicator's deadline
+            if dd.comm is not None and dd.comm.status() == 0:
+                dd.comm.abort()
+            raise
         finally:
             # also when a fit or a helper task raised: no helper work outlives the call
             helper.shutdown(wait=True, cancel_futures=True)

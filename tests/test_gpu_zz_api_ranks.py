@@ -42,34 +42,55 @@ def _fit(timings=None, **extra):
     return out
 
 
-def _api_worker(rank, world, port, out_dir):
+def _api_worker(rank, world, port, out_dir, comm="torch", fault=None):
     import faulthandler
     import sys
+    import time
     # a hung rank shows where, well before the test's own deadline (90 s) and any runner limit
     faulthandler.dump_traceback_later(60, exit=True, file=sys.stderr)
+    if comm == "host":                   # the library's C loop with its host-staged communicator
+        os.environ["PERT_NATIVE_COMM"] = "host"
+    if fault is not None:
+        os.environ["PERT_COMM_FAULT_AT"] = fault
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{}".format(port), rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
         tm = {}
+        if fault is not None:
+            from scdna_replication_tools_amd._native import CommError
+            try:
+                _fit(timings=tm, device="cuda:0")
+                got = {"raised": -1}
+            except CommError as e:
+                got = {"raised": e.code}
+            got["t_raise"] = time.time()
+            torch.save(got, os.path.join(out_dir, "fault{}.pt".format(rank)))
+            return
+        from scdna_replication_tools.pert_model import pert_infer_scRT
+        launched = {}
+        orig = pert_infer_scRT.run_pert_model
+
+        def run(self):                    # the iterations each fit queued on this rank
+            try:
+                return orig(self)
+            finally:
+                launched.update(self.launched)
+        pert_infer_scRT.run_pert_model = run
         cn_s, supp_s, cn_g, supp_g = _fit(timings=tm, device="cuda:0")
         cols = ["model_cn_state", "model_rep_state", "model_tau", "model_u", "model_rho"]
         torch.save({"s": torch.as_tensor(cn_s[cols].to_numpy(np.float64)),
                     "g": torch.as_tensor(cn_g[cols].to_numpy(np.float64)),
                     "loss_s": torch.as_tensor(supp_s.loc[supp_s.param == "loss_s", "value"].to_numpy(np.float64)),
                     "loss_g": torch.as_tensor(supp_s.loc[supp_s.param == "loss_g", "value"].to_numpy(np.float64)),
-                    "timings": tm},
+                    "timings": tm, "launched": launched},
                    os.path.join(out_dir, "api{}.pt".format(rank)))
     finally:
         dist.destroy_process_group()
 
 
-def test_run_pert_model_two_ranks_match_single_rank(tmp_path):
-    """The public entry point under torch.distributed (pert_model._Dist): each fit is
-    cell-sharded over the two ranks with the all-reduce per step, every rank returns the full
-    output tables -- equal to the single-process fit's (losses to summation-order noise,
-    calls and per-cell sites)."""
+def _spawn(tmp_path, comm, fault=None):
     import time
-    ctx = mp.spawn(_api_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=False)
+    ctx = mp.spawn(_api_worker, args=(2, _free_port(), str(tmp_path), comm, fault), nprocs=2, join=False)
     deadline = time.time() + 90           # bounded: a hung rank fails the test instead of the suite
     while not ctx.join(timeout=5):
         if time.time() > deadline:
@@ -77,6 +98,30 @@ def test_run_pert_model_two_ranks_match_single_rank(tmp_path):
                 if p.is_alive():
                     p.kill()
             pytest.fail("the two ranks did not finish within 90 s")
+
+
+def test_fault_on_rank1_stops_rank0_through_the_library_loop(tmp_path):
+    """PERT_COMM_FAULT_AT=1:30: rank 1's all-reduce call 30 (inside step 1's fit) fails; rank 1
+    raises CommError, raises the abort word, and rank 0 -- waiting on its stream inside the C
+    loop -- raises CommError too, within 10 s, instead of hanging."""
+    from scdna_replication_tools_amd import _native as nat
+    _spawn(tmp_path, "host", fault="1:30")
+    r = [torch.load(str(tmp_path / "fault{}.pt".format(i)), weights_only=True) for i in range(2)]
+    assert r[1]["raised"] == nat.E_COMM_FAULT, r[1]
+    assert r[0]["raised"] == nat.E_COMM_ABORTED, r[0]
+    assert abs(r[0]["t_raise"] - r[1]["t_raise"]) < 10.0
+    print("rank 0 raised {:.3f} s after rank 1".format(r[0]["t_raise"] - r[1]["t_raise"]))
+
+
+@pytest.mark.parametrize("comm", ["torch", "host"])
+def test_run_pert_model_two_ranks_match_single_rank(tmp_path, comm):
+    """The public entry point under torch.distributed (pert_model._Dist): each fit is
+    cell-sharded over the two ranks with the all-reduce per step, every rank returns the full
+    output tables -- equal to the single-process fit's (losses to summation-order noise,
+    calls and per-cell sites).  comm="torch": the per-step Python loop over gloo; "host": the
+    product's one-call C loop (pert_svi_run_sharded) over the library's host-staged
+    communicator, the loop an RCCL node runs -- and both ranks queue the same chunks."""
+    _spawn(tmp_path, comm)
     r = [torch.load(str(tmp_path / "api{}.pt".format(i)), weights_only=True) for i in range(2)]
     tm1 = {}
     cn_s, supp_s, cn_g, supp_g = _fit(timings=tm1)
@@ -102,3 +147,4 @@ def test_run_pert_model_two_ranks_match_single_rank(tmp_path):
         assert len(r[i]["loss_s"]) == len(ls) and len(r[i]["loss_g"]) == len(lg)
         np.testing.assert_allclose(r[i]["loss_s"].numpy(), ls, rtol=1e-6)
         np.testing.assert_allclose(r[i]["loss_g"].numpy(), lg, rtol=1e-6)
+    assert r[0]["launched"] == r[1]["launched"] and len(r[0]["launched"]) == 3, r[0]["launched"]

@@ -79,6 +79,32 @@ def test_argument_validation_without_launch(nat):
     assert rc == 1                      # PERT_E_ARG (null pointers)
 
 
+def test_host_comm_refuses_bad_arguments_and_times_out_alone(nat):
+    """pert_comm_init_host: argument checks, and a rank whose peers never attach returns
+    PERT_E_COMM_TIMEOUT after its deadline and leaves no segment in /dev/shm (no GPU needed:
+    the attach comes before any HIP call)."""
+    import ctypes
+    import os
+    import time
+    lib = nat.lib_nogil()
+    h = ctypes.c_void_p()
+    name = "/pert-test-{}".format(os.getpid()).encode()
+    assert lib.pert_comm_init_host(None, 2, 0, 16, 1.0, ctypes.byref(h)) == 1
+    assert lib.pert_comm_init_host(b"no-slash", 2, 0, 16, 1.0, ctypes.byref(h)) == 1
+    assert lib.pert_comm_init_host(name, 0, 0, 16, 1.0, ctypes.byref(h)) == 1
+    assert lib.pert_comm_init_host(name, 2, 2, 16, 1.0, ctypes.byref(h)) == 1
+    assert lib.pert_comm_init_host(name, 2, 0, 0, 1.0, ctypes.byref(h)) == 1
+    assert lib.pert_comm_init_host(name, 2, 0, 16, 0.0, ctypes.byref(h)) == 1
+    t0 = time.perf_counter()
+    assert lib.pert_comm_init_host(name, 2, 0, 16, 0.3, ctypes.byref(h)) == nat.E_COMM_TIMEOUT
+    assert 0.25 < time.perf_counter() - t0 < 5.0
+    assert not h.value
+    assert not os.path.exists("/dev/shm" + name.decode())
+    assert lib.pert_comm_status(None) == 1 and lib.pert_comm_abort(None, 6) == 1
+    assert lib.pert_comm_set_watchdog(None, None, 1.0) == 1 and lib.pert_comm_inject_fault(None, 0) == 1
+    assert lib.pert_comm_wait_event(None, None) == 1
+
+
 def test_comm_loads_rccl_and_refuses_bad_arguments(nat):
     """pert_comm_load finds the RCCL this process already uses (torch's) and resolves its
     symbols; a unique id is made without a GPU; the sharded loop entry points refuse a null

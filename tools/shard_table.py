@@ -1,6 +1,6 @@
 """One-lease strong-scaling table from bench.py lines.
 
-Reads the JSON lines tools/r05d.sh collected (each a bench.py run: the 10 k-cell C4 step on one
+Reads the JSON lines tools/shard_runs.sh collects (each a bench.py run: the 10 k-cell C4 step on one
 rank, and the per-rank shard of an N-GPU run -- 10 k / N cells -- with the library's RCCL
 all-reduce at world 1) and prints, per repetition, the projected N-GPU efficiency
 T(10 k) / (N x T(10 k / N)) from the timed steps (HIP events on every 5th pass) and from the

@@ -333,6 +333,13 @@ def main():
                          "(pert_comm, queued inside the C loop; the default on N > 1 over nccl, and at N = 1 "
                          "it times the sharded step with a one-rank all-reduce), 'torch' = torch.distributed "
                          "per step from Python")
+    ap.add_argument("--comm-overlap", type=int, default=0,
+                    help="1: the sharded step split so the all-reduce overlaps the per-cell finalize on a side "
+                         "stream (pert_comm_allreduce_async); 0 (default; faster on ROCm 7.2): finalize, "
+                         "all-reduce, Adam in sequence")
+    ap.add_argument("--comm-delay-us", type=float, default=0.0,
+                    help="a kernel spinning this long with every all-reduce (stand-in for an 8-rank ring's "
+                         "latency at N = 1; measurement only)")
     ap.add_argument("--cpu-cells", type=int, default=640)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -412,6 +419,8 @@ def main():
             comm_error = "{}: {}".format(type(e).__name__, e)
             print("bench: the library's RCCL communicator failed ({}); all-reducing through "
                   "torch.distributed".format(comm_error), file=sys.stderr, flush=True)
+    if comm is not None:
+        comm.set_options(overlap=bool(args.comm_overlap), delay_us=args.comm_delay_us)
     allreduce = comm.allreduce if comm is not None else make_allreduce()
     comm_desc = ("rccl: the library's own communicator, all-reduce queued inside the C loop (pert_svi_run_sharded)"
                  if comm is not None else "torch.distributed all_reduce per step from Python{}".format(
@@ -537,6 +546,8 @@ def main():
             "config": {"workload": desc, "config": args.config, "cells": n_total, "bins": L, "P": P,
                        "K": K, "cn_prior": prior_desc, "parallelism": "cell-sharded x{}".format(world),
                        "bins_per_tile": shard.bins_per_tile, "fit": args.fit, "allreduce": comm_desc,
+                       "comm_overlap": bool(args.comm_overlap) if comm is not None else None,
+                       "comm_delay_us": args.comm_delay_us if comm is not None else None,
                        "timed_loop": ("pert_svi_run{}: the whole loop in one GIL-free C call, no timing "
                                       "events".format("_sharded" if comm is not None else "")
                                       if comm is not None or allreduce is None

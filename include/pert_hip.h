@@ -210,6 +210,13 @@ int pert_obs_pass(const pert_problem* prob, pert_state* st, hipStream_t stream);
  * -> grad_cell (local) and grad_shared (local partial sums incl. the loss in slot n_shared).
  * One launch: its last workgroup to finish adds the global sums. */
 int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream);
+/* pert_finalize split in two for a sharded step, so the shared block's all-reduce overlaps the
+ * per-cell work: _shared writes grad_shared (local sums and loss) from the bin partials, the
+ * pass's ELBO / d/da partials and the priors' terms (parameters only); _cells writes grad_cell
+ * from each cell's partial rows and the u / beta / tau priors.  Together they write exactly
+ * what pert_finalize writes; pert_adam follows both. */
+int pert_finalize_shared(const pert_problem* prob, pert_state* st, hipStream_t stream);
+int pert_finalize_cells(const pert_problem* prob, pert_state* st, hipStream_t stream);
 
 /* Adam (torch.optim.Adam semantics, betas (0.8, 0.99)) on the packed params with
  * grad_shared (already all-reduced) and grad_cell. */
@@ -292,6 +299,18 @@ int pert_comm_wait_event(pert_comm* comm, hipEvent_t ev);
 /* Test hook: this rank's all-reduce call number `at_call` (0-based, -1 = never) fails at
  * queue time with PERT_E_COMM_FAULT, as a rank's launch failure would. */
 int pert_comm_inject_fault(pert_comm* comm, int64_t at_call);
+/* overlap (default 0, measured slower on ROCm 7.2: DESIGN.md section 6): pert_svi_run_sharded's
+ * three-launch step runs split -- pert_finalize_shared,
+ * the all-reduce on the comm's side stream (pert_comm_allreduce_async) while the fit's stream runs
+ * pert_finalize_cells, then pert_comm_join + pert_adam; 0: pert_finalize, the all-reduce,
+ * pert_adam on one stream.  delay_us > 0 (measurement only): every all-reduce also
+ * runs a kernel spinning that long on its stream, a stand-in for an 8-rank ring's latency. */
+int pert_comm_set_options(pert_comm* comm, int32_t overlap, double delay_us);
+int pert_comm_overlap(const pert_comm* comm);
+/* The all-reduce queued on the comm's side stream after the work already queued on `stream`
+ * (overlap 0: on `stream` itself); pert_comm_join makes `stream` wait for it. */
+int pert_comm_allreduce_async(pert_comm* comm, const double* send, double* recv, int64_t n, hipStream_t stream);
+int pert_comm_join(pert_comm* comm, hipStream_t stream);
 int pert_comm_destroy(pert_comm* comm);
 /* recv = sum over ranks of send (fp64, n elements; send == recv allowed), queued on stream. */
 int pert_comm_allreduce_sum_f64(pert_comm* comm, const double* send, double* recv, int64_t n,

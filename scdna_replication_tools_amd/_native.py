@@ -31,7 +31,8 @@ EXPORTED_SYMBOLS = (
     "pert_svi_run", "pert_comm_load", "pert_comm_unique_id", "pert_comm_init", "pert_comm_destroy",
     "pert_comm_allreduce_sum_f64", "pert_svi_steps_sharded", "pert_svi_run_sharded", "pert_version",
     "pert_comm_init_host", "pert_comm_set_watchdog", "pert_comm_abort", "pert_comm_status", "pert_comm_wait_event",
-    "pert_comm_inject_fault",
+    "pert_comm_inject_fault", "pert_finalize_shared", "pert_finalize_cells", "pert_comm_set_options",
+    "pert_comm_overlap", "pert_comm_allreduce_async", "pert_comm_join",
 )
 
 # include/pert_hip.h status codes of a sharded fit's communicator
@@ -193,6 +194,12 @@ def load(path: str, gil: bool = True):
     handle.pert_comm_status.argtypes = [c_void_p]
     handle.pert_comm_wait_event.argtypes = [c_void_p, c_void_p]
     handle.pert_comm_inject_fault.argtypes = [c_void_p, i64]
+    handle.pert_comm_set_options.argtypes = [c_void_p, i32, ctypes.c_double]
+    handle.pert_comm_overlap.argtypes = [c_void_p]
+    handle.pert_comm_allreduce_async.argtypes = [c_void_p, c_void_p, c_void_p, i64, c_void_p]
+    handle.pert_comm_join.argtypes = [c_void_p, c_void_p]
+    handle.pert_finalize_shared.argtypes = [POINTER(PertProblem), POINTER(PertState), c_void_p]
+    handle.pert_finalize_cells.argtypes = [POINTER(PertProblem), POINTER(PertState), c_void_p]
     handle.pert_svi_steps_sharded.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams), fp,
                                               fp, i32, i32, i32, c_void_p, c_void_p, c_void_p, c_void_p]
     handle.pert_svi_run_sharded.argtypes = [POINTER(PertProblem), POINTER(PertState), POINTER(PertAdamHparams), fp,

@@ -151,6 +151,14 @@ struct pert_comm {
   double timeout_s = kDefaultTimeoutS;
   int64_t fault_at = -1;                // test hook: the all-reduce call of this index fails
   int64_t n_calls = 0;                  // all-reduce calls queued
+  // the split step's overlap (pert_comm_allreduce_async / pert_comm_join): a side stream and
+  // two events, made on first use on the current device.  Off by default: on ROCm 7.2 each
+  // cross-stream hop costs ~14 us (tools/xstream_probe.py) and RCCL on the side stream made the
+  // 1,250-cell step 0.42 -> 0.69 ms, more than the per-cell work it hides
+  int32_t overlap = 0;
+  int64_t delay_ticks = 0;              // stand-in latency (pert_comm_set_options), 100 MHz ticks
+  hipStream_t side = nullptr;
+  hipEvent_t ev_sums = nullptr, ev_done = nullptr;
   // host backend
   double* pin_send = nullptr;
   double* pin_recv = nullptr;
@@ -186,6 +194,15 @@ int poll_failure(pert_comm* c) {
   }
   return PERT_OK;
 }
+
+// the stand-in for a ring's latency (pert_comm_set_options): one wave spinning on the
+// device's constant 100 MHz clock
+__global__ void delay_kernel(int64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(1);
+}
+
+int hip_rc(hipError_t e) { return e == hipSuccess ? PERT_OK : PERT_E_HIP_BASE + (int)e; }
 
 struct HostCall {
   pert_comm* c;
@@ -369,9 +386,48 @@ int pert_comm_wait_event(pert_comm* c, hipEvent_t ev) {
   }
 }
 
+int pert_comm_set_options(pert_comm* c, int32_t overlap, double delay_us) {
+  if (!c || delay_us < 0.0) return PERT_E_ARG;
+  c->overlap = overlap ? 1 : 0;
+  c->delay_ticks = (int64_t)(delay_us * 100.0 + 0.5);
+  return PERT_OK;
+}
+
+int pert_comm_overlap(const pert_comm* c) { return c && c->overlap ? 1 : 0; }
+
+int pert_comm_allreduce_async(pert_comm* c, const double* send, double* recv, int64_t n, hipStream_t stream) {
+  if (!c) return PERT_E_ARG;
+  if (!c->overlap) return pert_comm_allreduce_sum_f64(c, send, recv, n, stream);
+  if (!c->side) {
+    int lo = 0, hi = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_sums, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming);
+    if (e != hipSuccess) return hip_rc(e);
+  }
+  int rc = hip_rc(hipEventRecord(c->ev_sums, stream));
+  if (rc == PERT_OK) rc = hip_rc(hipStreamWaitEvent(c->side, c->ev_sums, 0));
+  if (rc == PERT_OK) rc = pert_comm_allreduce_sum_f64(c, send, recv, n, c->side);
+  if (rc == PERT_OK) rc = hip_rc(hipEventRecord(c->ev_done, c->side));
+  return rc;
+}
+
+int pert_comm_join(pert_comm* c, hipStream_t stream) {
+  if (!c) return PERT_E_ARG;
+  if (!c->overlap || !c->side) return PERT_OK;
+  return hip_rc(hipStreamWaitEvent(stream, c->ev_done, 0));
+}
+
 int pert_comm_destroy(pert_comm* c) {
   if (!c) return PERT_OK;
   int rc = PERT_OK;
+  if (c->side) {
+    (void)hipStreamSynchronize(c->side);
+    (void)hipStreamDestroy(c->side);
+    (void)hipEventDestroy(c->ev_sums);
+    (void)hipEventDestroy(c->ev_done);
+  }
   if (c->kind == kKindRccl && c->nccl)
     rc = g_rccl.handle ? comm_status(g_rccl.destroy(c->nccl)) : PERT_E_COMM_UNAVAILABLE;
   if (c->pin_send) (void)hipHostFree(c->pin_send);
@@ -388,6 +444,11 @@ int pert_comm_allreduce_sum_f64(pert_comm* c, const double* send, double* recv, 
   if (call == c->fault_at) return PERT_E_COMM_FAULT;          // test hook (pert_comm_inject_fault)
   const int f = c->failed.load(std::memory_order_acquire);
   if (f) return f;
+  if (c->delay_ticks > 0) {
+    hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, stream, c->delay_ticks);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_rc(e);
+  }
   if (c->kind == kKindHost) {
     if (n > c->seg.max_n) return PERT_E_ARG;
     hipError_t e = hipMemcpyAsync(c->pin_send, send, sizeof(double) * n, hipMemcpyDeviceToHost, stream);

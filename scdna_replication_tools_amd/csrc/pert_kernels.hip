@@ -1201,6 +1201,17 @@ __global__ void __launch_bounds__(64) obs_pair_kernel(pert_problem pr, pert_stat
   }
 }
 
+// Adam of one packed parameter (torch.optim.Adam; the adam_kernel arithmetic)
+__device__ __forceinline__ void adam_one(const pert_state& st, const pert_adam_hparams& hp, int i, float g) {
+  float mm = st.adam_m[i], vv = st.adam_v[i];
+  mm = hp.beta1 * mm + (1.0f - hp.beta1) * g;
+  vv = hp.beta2 * vv + (1.0f - hp.beta2) * g * g;
+  const float denom = sqrtf(vv) * hp.inv_bc2_sqrt + hp.eps;
+  st.params[i] -= hp.step_size * mm / denom;
+  st.adam_m[i] = mm;
+  st.adam_v[i] = vv;
+}
+
 // ------------------------------------------------------------------------------------------
 // Per-cell and per-bin reductions + priors of the non-enumerated sites + the global sums,
 // one launch.  1024-thread workgroups = 64 items (lanes) x 16 groups (waves).  Blocks
@@ -1337,7 +1348,15 @@ __device__ __forceinline__ void cell_grads(int K1, bool step1, float c0, float u
 // block's per-library beta_stds / beta_means sums, ELBO and d/da into cellblk_part.
 // Everything wave 0 needs besides the sums (its cells' parameters, the per-library prior
 // table in LDS, the tile's ELBO / d/da partials) is requested before the partial loop.
-template <int K1T>
+// PART (the split finalize of a sharded step, pert_finalize_shared / pert_finalize_cells):
+//   kFinAll    both halves (pert_finalize);
+//   kFinShared only what the shared block needs -- the priors' per-library / ELBO terms
+//              (parameters only) and the tile's ELBO / d/da partials -- into cellblk_part;
+//   kFinCells  only the per-cell data sums + priors -> grad_cell, while the shared block is
+//              all-reduced (Adam then runs once both are done).
+constexpr int kFinAll = 0, kFinShared = 1, kFinCells = 2;
+
+template <int K1T, int PART = kFinAll>
 __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_state& st, int cb, int n_bt,
                                           bool stopped, double (*s_g)[64]) {
   constexpr int kCS = K1T + 1;
@@ -1374,7 +1393,7 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
   // the enumerated pass's ELBO / d/da sums of this cell tile, one bin tile per thread
   double wl = 0.0, wa = 0.0;
   const size_t bstride = (size_t)(pr.ldn / 64) * kBlkSlots;
-  if (!step1 && tid < n_bt) {
+  if (PART != kFinCells && !step1 && tid < n_bt) {
     const double* bp = st.blk_part + (size_t)tid * bstride + (size_t)cb * kBlkSlots;
     wl = bp[0];
     wa = bp[1];
@@ -1382,7 +1401,7 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
   double A[kCS];
 #pragma unroll
   for (int k = 0; k < kCS; ++k) A[k] = 0.0;
-  if (in_range) {
+  if (PART != kFinShared && in_range) {
     const float* __restrict__ cp = st.cell_part;
     const size_t tstride = (size_t)CS * N;
     for (int b0 = grp; b0 < n_bt; b0 += kFinG * kFinU) {
@@ -1403,7 +1422,7 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
         for (int k = 0; k < kCS; ++k) A[k] += (double)v[u][k];
     }
   }
-  if (!step1) {
+  if (PART != kFinCells && !step1) {
     for (int bt = tid + kFinBlock; bt < n_bt; bt += kFinBlock) {
       const double* bp = st.blk_part + (size_t)bt * bstride + (size_t)cb * kBlkSlots;
       wl += bp[0];
@@ -1441,7 +1460,7 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
   }
   CellGrads<K1T> cg;
   cell_grads<K1T>(K1, step1, (1.0f - lam) / lam, u, tau_z, mean_x, ploidy, bz, lbsd, lbmn, T, cg);
-  if (valid) {
+  if (PART != kFinShared && valid) {
     float* gc = st.grad_cell - lay.n_shared;
     gc[lay.off_u + n] = -cg.dU;
 #pragma unroll
@@ -1449,6 +1468,7 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
       if (k < K1) gc[lay.off_beta + k * N + n] = -cg.dB[k];
     gc[lay.off_tau + n] = -cg.dTauZ;
   }
+  if (PART == kFinCells) return;                           // (the shared half wrote the slots)
   const double lp = valid ? cg.lp : 0.0;
   float dzbs[K1T], dbm[K1T];
 #pragma unroll
@@ -1597,7 +1617,7 @@ __device__ void fin_global(const pert_problem& pr, const pert_state& st, int n_b
   st.grad_shared[lay.n_shared] = -elbo;                     // local loss (host adds constants)
 }
 
-template <int K1T>
+template <int K1T, int PART>
 __global__ void __launch_bounds__(kFinBlock) finalize_kernel(pert_problem pr, pert_state st, int n_cblk,
                                                              int n_bt, int n_ct, int n_blk) {
   // the device loop's stop flag is read first but tested only before the first store, so
@@ -1607,8 +1627,8 @@ __global__ void __launch_bounds__(kFinBlock) finalize_kernel(pert_problem pr, pe
   __shared__ int s_last;
   const int tid = threadIdx.x;
   if ((int)blockIdx.x >= n_cblk) fin_bins(pr, st, blockIdx.x - n_cblk, n_ct, stopped, s_g);
-  else fin_cells<K1T>(pr, st, blockIdx.x, n_bt, stopped, s_g);
-  if (stopped) return;
+  else fin_cells<K1T, PART>(pr, st, blockIdx.x, n_bt, stopped, s_g);
+  if (stopped || PART == kFinCells) return;                // (the cell half has no global sums)
   // Wave 0 wrote this block's outputs: publish them (agent-scope release), then count the
   // block in.  The last block to arrive acquires and runs the global sums, then re-arms
   // the counter for the next launch.
@@ -1660,17 +1680,6 @@ __device__ void loop_record(const pert_state& st) {
     st.loop_ctl[1] = reason;
     st.loop_ctl[0] = t;
   }
-}
-
-// Adam of one packed parameter (torch.optim.Adam; the adam_kernel arithmetic)
-__device__ __forceinline__ void adam_one(const pert_state& st, const pert_adam_hparams& hp, int i, float g) {
-  float mm = st.adam_m[i], vv = st.adam_v[i];
-  mm = hp.beta1 * mm + (1.0f - hp.beta1) * g;
-  vv = hp.beta2 * vv + (1.0f - hp.beta2) * g * g;
-  const float denom = sqrtf(vv) * hp.inv_bc2_sqrt + hp.eps;
-  st.params[i] -= hp.step_size * mm / denom;
-  st.adam_m[i] = mm;
-  st.adam_v[i] = vv;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2439,23 +2448,46 @@ int pert_obs_pass(const pert_problem* prob, pert_state* st, hipStream_t stream) 
   return hip_status(hipGetLastError());
 }
 
-int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream) {
-  if (!problem_ok(prob) || !st || !st->grad_shared || !st->grad_cell || !st->cellblk_part) return PERT_E_ARG;
+}  // extern "C"
+
+namespace {
+
+template <int PART>
+int launch_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream) {
   pert_state s2 = *st;
   s2.bins_per_tile = tile_bins(prob, st);
   const int lt = s2.bins_per_tile;
   const int n_ct = prob->kind == PERT_KIND_STEP1 ? obs_cell_tiles(prob) : enum_cell_tiles(prob, st);
   const int n_bt = (prob->L + lt - 1) / lt;
-  const int n_lblk = (prob->L + 63) / 64;
+  const int n_lblk = PART == kFinCells ? 0 : (prob->L + 63) / 64;
   const int n_cblk = (prob->N + 63) / 64;
   const int n_blk = prob->kind == PERT_KIND_STEP1 ? n_bt * n_ct : 0;   // observed pass only
   if (prob->K1 == 5)
-    hipLaunchKernelGGL(finalize_kernel<5>, dim3(n_cblk + n_lblk), dim3(kFinBlock), 0, stream, *prob, s2, n_cblk,
-                       n_bt, n_ct, n_blk);
-  else
-    hipLaunchKernelGGL(finalize_kernel<PERT_MAX_K1>, dim3(n_cblk + n_lblk), dim3(kFinBlock), 0, stream, *prob, s2,
+    hipLaunchKernelGGL((finalize_kernel<5, PART>), dim3(n_cblk + n_lblk), dim3(kFinBlock), 0, stream, *prob, s2,
                        n_cblk, n_bt, n_ct, n_blk);
+  else
+    hipLaunchKernelGGL((finalize_kernel<PERT_MAX_K1, PART>), dim3(n_cblk + n_lblk), dim3(kFinBlock), 0, stream,
+                       *prob, s2, n_cblk, n_bt, n_ct, n_blk);
   return hip_status(hipGetLastError());
+}
+
+}  // namespace
+
+extern "C" {
+
+int pert_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream) {
+  if (!problem_ok(prob) || !st || !st->grad_shared || !st->grad_cell || !st->cellblk_part) return PERT_E_ARG;
+  return launch_finalize<kFinAll>(prob, st, stream);
+}
+
+int pert_finalize_shared(const pert_problem* prob, pert_state* st, hipStream_t stream) {
+  if (!problem_ok(prob) || !st || !st->grad_shared || !st->cellblk_part) return PERT_E_ARG;
+  return launch_finalize<kFinShared>(prob, st, stream);
+}
+
+int pert_finalize_cells(const pert_problem* prob, pert_state* st, hipStream_t stream) {
+  if (!problem_ok(prob) || !st || !st->grad_cell || !st->cell_part) return PERT_E_ARG;
+  return launch_finalize<kFinCells>(prob, st, stream);
 }
 
 int pert_adam(const pert_problem* prob, pert_state* st, const pert_adam_hparams* hp, hipStream_t stream) {
@@ -2508,6 +2540,17 @@ int svi_steps(const pert_problem* prob, pert_state* st, const pert_adam_hparams*
     if (rc == PERT_OK)
       rc = enumerated ? pert_enum_pass(prob, &s, &h, PERT_MODE_STEP, stream) : pert_obs_pass(prob, &s, stream);
     mark(i, 1);
+    if (comm && pert_comm_overlap(comm)) {
+      // the split step: the shared block's sums first, its all-reduce on the comm's side
+      // stream while this stream runs the per-cell sums, then Adam (and the loss record) once
+      // both are done
+      if (rc == PERT_OK) rc = pert_finalize_shared(prob, &s_loc, stream);
+      if (rc == PERT_OK) rc = pert_comm_allreduce_async(comm, grad_local, st->grad_shared, n_sum, stream);
+      if (rc == PERT_OK) rc = pert_finalize_cells(prob, &s, stream);
+      if (rc == PERT_OK) rc = pert_comm_join(comm, stream);
+      if (rc == PERT_OK) rc = pert_adam(prob, &s, &h, stream);
+      continue;
+    }
     if (rc == PERT_OK) rc = pert_finalize(prob, comm ? &s_loc : &s, stream);
     if (comm) all_reduce();
     if (rc == PERT_OK) rc = pert_adam(prob, &s, &h, stream);

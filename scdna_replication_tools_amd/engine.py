@@ -389,6 +389,15 @@ class PertComm:
                                                         torch.cuda.current_stream(t.device).cuda_stream),
                   "pert_comm_allreduce_sum_f64")
 
+    def set_options(self, overlap: bool = False, delay_us: float = 0.0) -> None:
+        """overlap: the sharded loop's split step (the shared block's all-reduce on a side
+        stream beside the per-cell finalize; off by default -- the cross-stream hops cost more
+        than they hide on ROCm 7.2); delay_us > 0: a kernel
+        spinning that long with every all-reduce -- a stand-in for an 8-rank ring's latency
+        on a one-GPU box (measurement only)."""
+        nat.check(self.lib.pert_comm_set_options(self.handle, 1 if overlap else 0, float(delay_us)),
+                  "pert_comm_set_options")
+
     def status(self) -> int:
         """0, or the first failure this rank has seen (its own, or a peer's abort)."""
         return int(self.lib.pert_comm_status(self.handle))

@@ -1,7 +1,8 @@
 """GPU: the library's own RCCL communicator (pert_comm, include/pert_hip.h) driving a sharded
 fit's whole SVI loop in C (pert_svi_run_sharded / pert_svi_steps_sharded: reductions into the
 shard's grad_local, the all-reduce queued on the fit's stream, Adam) against the same sharded
-step driven per iteration from Python (PertShard with a Python all-reduce).  One GPU, so the
+step driven per iteration from Python (PertShard with a Python all-reduce; the unsplit
+pert_finalize + pert_adam sequence).  One GPU, so the
 communicator is a one-rank RCCL world (a sum over one rank is the identity): both loops run
 the same kernels on the same state, and the loss traces, the stopping iteration and the final
 parameters must be identical bit for bit.  The multi-GPU bench runs the same path at N = 2..8.
@@ -54,9 +55,15 @@ def test_comm_allreduce_world1_is_identity(comm):
         (time.perf_counter() - t0) / n * 1e6))
 
 
-@pytest.mark.parametrize("kind,fused", [("step2", False), ("step2", True), ("step3", True), ("step1p", False)])
-@pytest.mark.parametrize("events", [False, True])
-def test_native_sharded_loop_matches_python_sharded_loop(comm, kind, fused, events):
+# overlap: the split step (pert_finalize_shared, the all-reduce on the comm's side stream beside
+# pert_finalize_cells_adam, pert_adam_shared) against the Python loop's pert_finalize + pert_adam;
+# delay: with a 20 us stand-in kernel in every all-reduce
+@pytest.mark.parametrize("kind,fused", [("step2", False), ("step2", True), ("step3", True), ("step1p", False),
+                                        ("step3", False)])
+@pytest.mark.parametrize("events,overlap,delay", [(False, True, 0.0), (True, True, 0.0), (False, False, 0.0),
+                                                  (True, False, 20.0), (False, True, 20.0)])
+def test_native_sharded_loop_matches_python_sharded_loop(comm, kind, fused, events, overlap, delay):
+    comm.set_options(overlap=overlap, delay_us=delay)
     prob, kw, z = make_problem(kind, seed=4)
     a = _shard(kind, kw, z, fused=fused, comm=comm)
     b = _shard(kind, kw, z, fused=fused, allreduce=lambda t: None)     # per-iteration Python loop
@@ -72,3 +79,4 @@ def test_native_sharded_loop_matches_python_sharded_loop(comm, kind, fused, even
         assert np.array_equal(sa[k], sb[k]), k
     if events:
         assert len(a.pass_events) >= len(la) // 3
+    comm.set_options()

@@ -14,6 +14,7 @@
 #   trace            rocprofv3 --kernel-trace --stats of the default bench
 #   pmc              tools/profile.sh's counter passes (one --pmc run each) + summary
 #   shard-table      tools/shard_runs.sh + shard_table.py (per-rank shards of C4 / C5 against the whole step)
+#   overlap-ab       tools/overlap_ab.sh (the sharded step's all-reduce overlap, with a 20 us stand-in)
 #   fullfit-c4       tools/fullfit_bench.py --config c4
 #   fullfit-c1       bench.py --fullfit-c1
 set -euo pipefail
@@ -22,7 +23,7 @@ R=$(pwd)
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 T="timeout -k 10"
-PYT="python -u -m pytest -x -v --timeout 150 --timeout-method thread"
+PYT="python -u -m pytest -x -v -rP --timeout 150 --timeout-method thread"
 for STEP in "$@"; do
   echo "[lease $TAG] $STEP $(date +%T)"
   case $STEP in
@@ -36,6 +37,7 @@ for STEP in "$@"; do
     trace) (cd /tmp && export TMPDIR=/tmp && $T 400 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/trace" -o run -- python3 "$R/bench.py" --no-cpu-baseline > "$OUT/trace.log" 2>&1) ;;
     pmc) $T 1000 bash tools/profile.sh "$TAG" ;;
+    overlap-ab) $T 1100 bash tools/overlap_ab.sh "$TAG" 2 > "$OUT/overlap_ab.log" 2>&1 ;;
     shard-table) $T 900 bash tools/shard_runs.sh "$TAG" 2 > "$OUT/shard_table.log" 2>&1 ;;
     fullfit-c4) $T 400 python tools/fullfit_bench.py --config c4 --cpu-sample-cells 0 > "$OUT/fullfit_c4.json" \
                   2> "$OUT/fullfit_c4.log" ;;

@@ -293,9 +293,10 @@ int pert_comm_abort(pert_comm* comm, int32_t code);
 /* PERT_OK, or the first failure seen by this rank (its own, or a peer's abort). */
 int pert_comm_status(pert_comm* comm);
 /* Wait for `ev` (recorded on the fit's stream) polling the abort word, RCCL's async error and
- * the deadline; on failure aborts the comm and returns the failure.  comm == NULL: blocking
- * hipEventSynchronize. */
-int pert_comm_wait_event(pert_comm* comm, hipEvent_t ev);
+ * the deadline; on failure aborts the comm and returns the failure.  eager: poll without
+ * sleeping (a wait whose end the caller's latency includes).  comm == NULL: hipEventSynchronize,
+ * or with eager a poll. */
+int pert_comm_wait_event(pert_comm* comm, hipEvent_t ev, int32_t eager);
 /* Test hook: this rank's all-reduce call number `at_call` (0-based, -1 = never) fails at
  * queue time with PERT_E_COMM_FAULT, as a rank's launch failure would. */
 int pert_comm_inject_fault(pert_comm* comm, int64_t at_call);

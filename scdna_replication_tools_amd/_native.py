@@ -192,7 +192,7 @@ def load(path: str, gil: bool = True):
     handle.pert_comm_set_watchdog.argtypes = [c_void_p, c_char_p, ctypes.c_double]
     handle.pert_comm_abort.argtypes = [c_void_p, i32]
     handle.pert_comm_status.argtypes = [c_void_p]
-    handle.pert_comm_wait_event.argtypes = [c_void_p, c_void_p]
+    handle.pert_comm_wait_event.argtypes = [c_void_p, c_void_p, i32]
     handle.pert_comm_inject_fault.argtypes = [c_void_p, i64]
     handle.pert_comm_set_options.argtypes = [c_void_p, i32, ctypes.c_double]
     handle.pert_comm_overlap.argtypes = [c_void_p]

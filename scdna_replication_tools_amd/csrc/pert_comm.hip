@@ -360,17 +360,21 @@ int pert_comm_abort(pert_comm* c, int32_t code) {
   return PERT_OK;
 }
 
-int pert_comm_wait_event(pert_comm* c, hipEvent_t ev) {
+int pert_comm_wait_event(pert_comm* c, hipEvent_t ev, int32_t eager) {
   if (!ev) return PERT_E_ARG;
-  if (!c) {
+  if (!c && !eager) {
     const hipError_t e = hipEventSynchronize(ev);
     return e == hipSuccess ? PERT_OK : PERT_E_HIP_BASE + (int)e;
   }
   const double t0 = now_s();
   for (int64_t k = 0;; ++k) {
     const hipError_t q = hipEventQuery(ev);
-    if (q == hipSuccess) return poll_failure(c);
+    if (q == hipSuccess) return c ? poll_failure(c) : PERT_OK;
     if (q != hipErrorNotReady) return PERT_E_HIP_BASE + (int)q;
+    if (!c) {                                   // eager, no comm: poll, yielding the core
+      if (k >= 256) sched_yield();
+      continue;
+    }
     int rc = poll_failure(c);
     if (rc == PERT_OK && (k & 63) == 63 && now_s() - t0 > c->timeout_s) {
       fail(c, PERT_E_COMM_TIMEOUT);
@@ -382,7 +386,8 @@ int pert_comm_wait_event(pert_comm* c, hipEvent_t ev) {
       (void)pert_comm_abort(c, rc);
       return rc;
     }
-    backoff(k);
+    if (eager && k >= 256) sched_yield();
+    else backoff(k);
   }
 }
 

@@ -2608,7 +2608,7 @@ int svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hparams* h
   hipEvent_t ev[65];
   if (ring > 64) return PERT_E_ARG;
   int made = 0;
-  int rc = take_events(ring + (comm ? 1 : 0), ev, &made);
+  int rc = take_events(ring + 1, ev, &made);
   int waited = 0;                              // chunks whose records have been looked at
   bool stop_seen = false;
   int c = 0;
@@ -2618,7 +2618,7 @@ int svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hparams* h
   // Sharded, a wait polls the communicator (a peer's abort, RCCL's async error, a deadline)
   // instead of blocking, so a failed rank cannot leave the others waiting forever.
   auto look = [&](int k) {
-    rc = rc == PERT_OK ? pert_comm_wait_event(comm, ev[k % ring]) : rc;
+    rc = rc == PERT_OK ? pert_comm_wait_event(comm, ev[k % ring], 0) : rc;
     const int j1 = (k + 1) * chunk < n_iter ? (k + 1) * chunk : n_iter;
     for (int j = k * chunk; j < j1 && rc == PERT_OK; ++j)
       if (host_rec[2 * j + 1] >= 0.0) stop_seen = true;
@@ -2635,16 +2635,17 @@ int svi_run(const pert_problem* prob, pert_state* st, const pert_adam_hparams* h
     if (rc == PERT_OK) rc = hip_status(hipEventRecord(ev[c % ring], stream));
     if (rc == PERT_OK) *n_launched = j0 + n;
   }
-  if (comm) {
-    // every queued launch and copy, waited for under the watchdog; a failure on this rank
-    // raises the abort word the peers poll, and stops this rank's own collectives
-    if (rc == PERT_OK && made == ring + 1) {
-      rc = hip_status(hipEventRecord(ev[ring], stream));
-      if (rc == PERT_OK) rc = pert_comm_wait_event(comm, ev[ring]);
-    }
-    if (rc != PERT_OK) (void)pert_comm_abort(comm, rc);
+  // every queued launch and copy, the last ones polled for rather than slept on (a blocking
+  // wait's wake-up was 35-120 us of every call's fixed cost, profiles/r06e); sharded, under the
+  // watchdog -- a failure on this rank raises the abort word the peers poll and stops this
+  // rank's own collectives
+  if (rc == PERT_OK && made == ring + 1) {
+    if (c >= 2 && waited < c - 1) rc = pert_comm_wait_event(comm, ev[(c - 2) % ring], 0);   // all but the last chunk
+    if (rc == PERT_OK) rc = hip_status(hipEventRecord(ev[ring], stream));
+    if (rc == PERT_OK) rc = pert_comm_wait_event(comm, ev[ring], 1);
   }
-  const hipError_t e = hipStreamSynchronize(stream);     // every queued launch and copy
+  if (comm && rc != PERT_OK) (void)pert_comm_abort(comm, rc);
+  const hipError_t e = hipStreamSynchronize(stream);     // (drained: returns at once)
   if (rc == PERT_OK) rc = hip_status(e);
   give_events(made, ev);
   return rc;

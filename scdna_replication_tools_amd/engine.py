@@ -1043,6 +1043,21 @@ class PertShard:
             self._ctl_init = torch.tensor([-1, 0], dtype=torch.int32, device=self.device)
         return self._loop_bufs
 
+    def _adam_schedule(self, t0: int, n: int):
+        """Adam's bias-corrected step sizes of steps t0+1 .. t0+n as _set_hparams computes them
+        (``lr / (1 - b1^t)``, ``1 / sqrt(1 - b2^t)``, Python floats cast to fp32), from a table
+        kept on the shard (a fit's call no longer loops over its steps in Python)."""
+        tab = self.__dict__.get("_adam_tab")
+        if tab is None or tab[0].shape[0] < t0 + n + 1:
+            cap = 1 << max(10, (t0 + n).bit_length())
+            b1, b2 = self.betas
+            ss = np.zeros(cap + 1, dtype=F32)
+            ib = np.zeros(cap + 1, dtype=F32)
+            ss[1:] = [self.lr / (1.0 - b1 ** t) for t in range(1, cap + 1)]
+            ib[1:] = [1.0 / math.sqrt(1.0 - b2 ** t) for t in range(1, cap + 1)]
+            tab = self._adam_tab = (ss, ib)
+        return tab[0][t0 + 1:t0 + n + 1], tab[1][t0 + 1:t0 + n + 1]
+
     def _timing_event(self):
         """A timing event from the pool reserve_svi fills (created and recorded once, so its HIP
         event exists), or a new one."""
@@ -1059,6 +1074,7 @@ class PertShard:
         call (run_pert_model computes the trajectory on its helper thread during the prep;
         bench.py calls this before its timed region)."""
         self._loop_buffers(int(n))
+        self._adam_schedule(self.t, int(n))
         if self.pi_block is not None:
             self.pi_block._cache(self.t + int(n) + 1)
         if self.pass_events is not None:            # the timing events a run_svi(n) will record
@@ -1111,9 +1127,7 @@ class PertShard:
         pending = []
         try:
             if native:
-                ts = range(t0 + 1, t0 + n + 1)
-                ss = np.array([self.lr / (1.0 - b1 ** t) for t in ts], dtype=F32)         # as _set_hparams
-                ib = np.array([1.0 / math.sqrt(1.0 - b2 ** t) for t in ts], dtype=F32)
+                ss, ib = self._adam_schedule(t0, n)
                 evp, sampled = None, []
                 if self.pass_events is not None:
                     ptrs = [None] * (2 * n)
@@ -1133,6 +1147,16 @@ class PertShard:
                         self._stream()), "pert_svi_run")
                 launched = int(nl.value)
                 self.last_launched = launched
+                # the stop from the copied records (every launched iteration's record is in
+                # pinned memory once the call returns; the first marked one is the stop --
+                # loop_ctl[0] -- and a NaN loss there is reason 2), no device read-back
+                marks = host[:launched, 1]
+                hit = torch.nonzero(marks >= 0)
+                if hit.numel():
+                    j = int(hit[0, 0])
+                    c = (j, 2 if math.isnan(float(host[j, 0])) else 1)
+                else:
+                    c = (-1, 0)
                 if self.pass_events is not None:       # (iterations never queued recorded nothing)
                     self.pass_events.extend((e0, e1) for i, e0, e1 in sampled if i < launched)
                 n = 0                              # nothing left for the per-iteration loop below
@@ -1153,7 +1177,8 @@ class PertShard:
                     stop_seen = stop_seen or bool((host[a:b, 1] >= 0).any())
                 if stop_seen:
                     break
-            c = ctl.cpu()                      # waits for every queued launch and copy
+            if not native:
+                c = ctl.cpu()                  # waits for every queued launch and copy
         finally:
             st.loop_ctl = st.loop_rec = st.loss_offset = None
             st.step = 0

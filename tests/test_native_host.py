@@ -102,7 +102,7 @@ def test_host_comm_refuses_bad_arguments_and_times_out_alone(nat):
     assert not os.path.exists("/dev/shm" + name.decode())
     assert lib.pert_comm_status(None) == 1 and lib.pert_comm_abort(None, 6) == 1
     assert lib.pert_comm_set_watchdog(None, None, 1.0) == 1 and lib.pert_comm_inject_fault(None, 0) == 1
-    assert lib.pert_comm_wait_event(None, None) == 1
+    assert lib.pert_comm_wait_event(None, None, 0) == 1
 
 
 def test_comm_loads_rccl_and_refuses_bad_arguments(nat):

@@ -94,10 +94,18 @@ PERT_HD float log1p_corr(float q, float inv_u) {
 }
 
 // Stirling remainder S(z) = 1/(12 z) - 1/(360 z^3) + 1/(1260 z^5): truncation error below
-// 1/(1680 z^7), 7.6e-9 at z = 5 (kAsymMin); the digamma series below (to 1/(252 z^6)) below
-// 1/(240 z^8), 1.1e-8 at z = 5.
-constexpr float kAsymMin = 5.0f;   // asymptotic series used for arguments >= kAsymMin
-constexpr float kShift = 4.0f;     // 1 <= d < kAsymMin is shifted by kShift (d + kShift >= kAsymMin)
+// 1/(1680 z^7), 2.7e-7 at z = 3 (kAsymMin); the digamma series below (to 1/(252 z^6)) below
+// 1/(240 z^8), 6.4e-7 at z = 3.  Over d in [3, 3.5] and every x the series' error in the terms
+// the kernels use is 1e-7 (Lambda) / 1.4e-6 (Psi) of the accuracy test's scale (5e-6 / 2e-5
+// allowed; at z = 5 it was 2e-9 / 4e-8).  Round 6 lowered the threshold from 5 (shift 4) to
+// 3 (shift 2): at 20 kb bins (C5: D = u omega (1-lam)/lam ~ 0.7) most chains of a wave run the
+// shift, and now with half its factors, fewer chains need it and more chain pairs run packed.
+#ifndef PERT_SHIFT_N
+#define PERT_SHIFT_N 2             // (A/B builds: -DPERT_SHIFT_N=4 is round 5's threshold 5 / shift 4)
+#endif
+constexpr int kShiftN = PERT_SHIFT_N;   // 1 <= d < kAsymMin is shifted by kShiftN (d + kShiftN >= kAsymMin)
+constexpr float kAsymMin = 1.0f + kShiftN;   // asymptotic series used for arguments >= kAsymMin
+constexpr float kShift = (float)kShiftN;
 PERT_HD float stirling_rem(float rz) {
   float rz2 = rz * rz;
   return rz * (0.0833333333333333333f - rz2 * (0.00277777777777777778f - rz2 * 0.000793650793650793651f));
@@ -195,17 +203,17 @@ PERT_HD void nb_asym_pair_direct(pf2 chi, float D, float x, float invx, float lo
   bc = chi * (psi + log1m_lam);
 }
 
-// 1 <= d < kAsymMin: shift by exactly kShift = 4 (d + 4 >= 5 for every d >= 1, so no per-lane
-// shift count) with the products A = prod_{i<4} (d+i), B = prod_{i<4} (d+x+i) and their
+// 1 <= d < kAsymMin: shift by exactly kShiftN = 2 (d + 2 >= 3 for every d >= 1, so no per-lane
+// shift count) with the products A = prod_{i<2} (d+i), B = prod_{i<2} (d+x+i) and their
 // d-derivatives carried along (one fma + one mul per factor, no per-factor reciprocal):
-//   lgamma(d+x) - lgamma(d) = [lgamma(d+4+x) - lgamma(d+4)] - log(B / A)
-//   psi(d+x) - psi(d)       = [psi(d+4+x) - psi(d+4)] - B'/B + A'/A
-// B / A <= (1 + x)^4, so nothing overflows for any count x < 4e9, and x = 0 gives exactly zero
+//   lgamma(d+x) - lgamma(d) = [lgamma(d+2+x) - lgamma(d+2)] - log(B / A)
+//   psi(d+x) - psi(d)       = [psi(d+2+x) - psi(d+2)] - B'/B + A'/A
+// B / A <= (1 + x)^2, so nothing overflows for any count x < 1e19, and x = 0 gives exactly zero
 // corrections (2 v_rcp + 1 v_log per shifted argument).
 PERT_HD void nb_shift(float d, float x, float& corr_l, float& corr_p) {
   float A = 1.0f, Ap = 0.0f, B = 1.0f, Bp = 0.0f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < kShiftN; ++i) {
     const float a = d + (float)i;
     const float b = a + x;
     Ap = Ap * a + A;

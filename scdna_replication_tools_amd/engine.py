@@ -941,8 +941,20 @@ class PertShard:
             held = [torch.empty(spacer, dtype=torch.uint8, device=self.device)] if spacer else []
             return tuple(torch.empty_like(self.z_pi) for _ in range(3)), held
 
-        best, times, held = placement_search(first, time_set, alloc, lambda: torch.cuda.mem_get_info(self.device)[0],
-                                             set_bytes, pattern_bytes, candidates)
+        try:
+            best, times, held = placement_search(first, time_set, alloc,
+                                                 lambda: torch.cuda.mem_get_info(self.device)[0],
+                                                 set_bytes, pattern_bytes, candidates)
+        except torch.cuda.OutOfMemoryError as e:
+            # another allocation on the device (a helper's step-3 work, another fit) took the
+            # room the tries assumed: keep the first set -- the search only ever speeds the
+            # pass up, results do not depend on it -- and give the tries back
+            self._set_pi_ptrs(*first)
+            torch.cuda.synchronize(self.device)
+            torch.cuda.empty_cache()
+            self.placement = {"candidates_ms": None, "chosen": 0, "error": "OutOfMemoryError: {}".format(
+                str(e).splitlines()[0][:200])}
+            return self.placement
         best_ms = min(times)
         if best is not first:
             for dst, src in zip(best, first):

@@ -55,3 +55,30 @@ def test_placement_default_applies_to_large_shards_only():
     from scdna_replication_tools_amd.engine import PertShard
     sh = PertShard(KIND_OF["step2"], init=init_constrained("step2", z), device="cuda", **kw)
     assert sh.z_pi.numel() < engine.PLACEMENT_MIN_FLOATS and sh.placement is None
+
+
+def test_placement_search_out_of_memory_keeps_the_first_set(monkeypatch):
+    """An allocation failure inside the search (another allocation on the device took the room)
+    leaves the shard on its first set, with the state and the library's pointers unchanged,
+    instead of failing the fit."""
+    from scdna_replication_tools_amd import engine
+    prob, kw, z = make_problem("step2", seed=6)
+    ref, _ = _shard("step2", kw, z, 0)
+    sh, before = _shard("step2", kw, z, 0)
+    ptrs = (sh.z_pi.data_ptr(), sh.m_pi.data_ptr(), sh.v_pi.data_ptr())
+
+    def failing(first, time_set, alloc, free_bytes, set_bytes, pattern_bytes, candidates):
+        time_set(first)
+        cand, _ = alloc(0)
+        time_set(cand)                     # the library now points at the try
+        raise torch.cuda.OutOfMemoryError("simulated")
+    monkeypatch.setattr(engine, "placement_search", failing)
+    rec = sh.choose_pi_placement(3)
+    assert rec["candidates_ms"] is None and "OutOfMemoryError" in rec["error"]
+    st = sh._state
+    assert (st.z_pi, st.m_pi, st.v_pi) == ptrs == (sh.z_pi.data_ptr(), sh.m_pi.data_ptr(), sh.v_pi.data_ptr())
+    for now, was in zip((sh.z_pi, sh.m_pi, sh.v_pi), before):
+        assert torch.equal(now, was)
+    la, _ = ref.run_svi(30, 10 ** 9, 0.0)
+    lb, _ = sh.run_svi(30, 10 ** 9, 0.0)
+    assert np.array_equal(np.asarray(la), np.asarray(lb))

@@ -22,6 +22,7 @@
 #include <math.h>
 #include <stddef.h>
 
+#include <algorithm>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -1235,6 +1236,49 @@ constexpr int kFinG = kFinBlock / 64;
 #endif
 __host__ __device__ constexpr int fin_slots(int n_libs, int K1) { return 2 * n_libs * K1 + 2; }
 
+// bin tiles per level-0 group: about sqrt(n_bt), so both levels stay short (C4: 13 x 14,
+// C5 at LT 32: 66 x 65)
+__device__ __forceinline__ int fused_g1(int n_bt) {
+  int g = 8;
+  while (g * g < n_bt) ++g;
+  return g;
+}
+__device__ __forceinline__ int fused_n_g1(int n_bt) { const int g = fused_g1(n_bt); return (n_bt + g - 1) / g; }
+
+// s[k] += sum_{j < n} p[j rs + k ps] for k < np, in j order; 4-8 rows x NP planes of loads in
+// flight per round trip (clamped indices, masked values: no guarded loads); coherent loads
+template <int NP>
+__device__ __forceinline__ void sum_rows(const float* __restrict__ p, size_t rs, size_t ps, int np, int n,
+                                         double (&s)[NP]) {
+  constexpr int R = NP >= 6 ? 4 : 8;                        // rows per round trip
+  for (int j0 = 0; j0 < n; j0 += R) {
+    float v[R][NP];
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        const int j = j0 + u;
+        const float x = ld_coh(p + (size_t)min(j, n - 1) * rs + (size_t)min(k, np - 1) * ps);
+        v[u][k] = (j < n && k < np) ? x : 0.0f;
+      }
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+#pragma unroll
+      for (int k = 0; k < NP; ++k) s[k] += (double)v[u][k];
+  }
+}
+
+// counters after finalize's arrival counter in cellblk_part: [n_ct][n_g1] group, [n_ct]
+// level-1, [n_bt] bin, [1] global
+__device__ __forceinline__ unsigned int* fused_counters(const pert_problem& pr, const pert_state& st) {
+  const int n_cblk = (pr.N + 63) / 64;
+  return reinterpret_cast<unsigned int*>(st.cellblk_part + (size_t)n_cblk * fin_slots(pr.n_libs, pr.K1) + 1);
+}
+
+__device__ __forceinline__ bool wave_flag(bool v) {
+  return __builtin_amdgcn_readfirstlane((int)v) != 0;
+}
+
 // ---- per-bin: d(-ELBO)/dz_rho   (rho ~ Beta(1,1) has zero log density, :574)
 __device__ __forceinline__ void fin_bins(const pert_problem& pr, const pert_state& st, int lb, int n_ct,
                                          bool stopped, double (*s_g)[64]) {
@@ -1356,9 +1400,17 @@ __device__ __forceinline__ void cell_grads(int K1, bool step1, float c0, float u
 //              all-reduced (Adam then runs once both are done).
 constexpr int kFinAll = 0, kFinShared = 1, kFinCells = 2;
 
+// Groups (n_cg > 1): a cell block's bin tiles are split over n_cg workgroups of kFinTPG tiles
+// (a genome of 20 kb bins has ~10^4 tiles: one workgroup per 64 cells walking them all left
+// the launch to 32 CUs at C5); each group's per-cell sums and ELBO / d/da sums go to a level-1
+// row (the rows after the bin tiles' in cell_part / blk_part, as pert_enum_step's), and the
+// group that arrives last adds the rows in group order and applies the priors.  n_cg == 1 is
+// the single-workgroup reduction, bit for bit.
+constexpr int kFinTPG = 128;
+
 template <int K1T, int PART = kFinAll>
 __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_state& st, int cb, int n_bt,
-                                          bool stopped, double (*s_g)[64]) {
+                                          bool stopped, double (*s_g)[64], int grp_c = 0, int n_cg = 1) {
   constexpr int kCS = K1T + 1;
   constexpr int kFinU = K1T <= 5 ? PERT_FIN_U : 1;   // bin tiles in flight per thread
   const int tid = threadIdx.x, lane = tid & 63, grp = tid >> 6;
@@ -1390,11 +1442,14 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
         lbmn[k] = step1 ? st.params[lay.off_bmeans + lib * K1 + k] : pr.beta_means[lib * K1 + k];
       }
   }
+  // this group's bin tiles [t0, t1) (all of them when n_cg == 1)
+  const int t0 = n_cg > 1 ? grp_c * kFinTPG : 0;
+  const int t1 = n_cg > 1 ? min(n_bt, t0 + kFinTPG) : n_bt;
   // the enumerated pass's ELBO / d/da sums of this cell tile, one bin tile per thread
   double wl = 0.0, wa = 0.0;
   const size_t bstride = (size_t)(pr.ldn / 64) * kBlkSlots;
-  if (PART != kFinCells && !step1 && tid < n_bt) {
-    const double* bp = st.blk_part + (size_t)tid * bstride + (size_t)cb * kBlkSlots;
+  if (PART != kFinCells && !step1 && tid < t1 - t0) {
+    const double* bp = st.blk_part + (size_t)(t0 + tid) * bstride + (size_t)cb * kBlkSlots;
     wl = bp[0];
     wa = bp[1];
   }
@@ -1404,16 +1459,16 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
   if (PART != kFinShared && in_range) {
     const float* __restrict__ cp = st.cell_part;
     const size_t tstride = (size_t)CS * N;
-    for (int b0 = grp; b0 < n_bt; b0 += kFinG * kFinU) {
+    for (int b0 = t0 + grp; b0 < t1; b0 += kFinG * kFinU) {
       float v[kFinU][kCS];
 #pragma unroll
       for (int u = 0; u < kFinU; ++u) {
         const int bt = b0 + u * kFinG;
-        const float* row = cp + (size_t)min(bt, n_bt - 1) * tstride + n;   // clamped, see fin_bins
+        const float* row = cp + (size_t)min(bt, t1 - 1) * tstride + n;   // clamped, see fin_bins
 #pragma unroll
         for (int k = 0; k < kCS; ++k) {
           const float x = row[(size_t)min(k, CS - 1) * N];
-          v[u][k] = (bt < n_bt && k < CS) ? x : 0.0f;
+          v[u][k] = (bt < t1 && k < CS) ? x : 0.0f;
         }
       }
 #pragma unroll
@@ -1423,7 +1478,7 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
     }
   }
   if (PART != kFinCells && !step1) {
-    for (int bt = tid + kFinBlock; bt < n_bt; bt += kFinBlock) {
+    for (int bt = t0 + tid + kFinBlock; bt < t1; bt += kFinBlock) {
       const double* bp = st.blk_part + (size_t)bt * bstride + (size_t)cb * kBlkSlots;
       wl += bp[0];
       wa += bp[1];
@@ -1451,6 +1506,43 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
   double tile_l = 0.0, tile_a = 0.0;
 #pragma unroll
   for (int g = 0; g < kFinG; ++g) { tile_l += s_g[g][0]; tile_a += s_g[g][1]; }
+  if (n_cg > 1) {
+    // level 1: this group's rows out (coherent stores), then count the group in; the last
+    // group of the cell block adds every group's rows in group order
+    const size_t tstride = (size_t)CS * N;
+    const bool blk = PART != kFinCells && !step1;
+    const size_t l1_stride = (size_t)(pr.ldn / 64) * kBlkSlots;
+    double* blk1 = st.blk_part + (size_t)n_bt * l1_stride + (size_t)cb * kBlkSlots;
+    float* lvl1 = st.cell_part + (size_t)n_bt * tstride + n;
+    if (PART != kFinShared && in_range) {
+      float* dst = lvl1 + (size_t)grp_c * tstride;
+#pragma unroll
+      for (int k = 0; k < kCS; ++k)
+        if (k < CS) st_coh(dst + (size_t)k * N, (float)T[k]);
+    }
+    if (blk && lane == 0) {
+      st_coh(blk1 + (size_t)grp_c * l1_stride, tile_l);
+      st_coh(blk1 + (size_t)grp_c * l1_stride + 1, tile_a);
+    }
+    publish_wait();
+    unsigned int* ctr = fused_counters(pr, st) + cb;        // (idle outside pert_enum_step)
+    bool last = false;
+    if (lane == 0) last = arrive(ctr, 1u) == (unsigned)(n_cg - 1);
+    if (!wave_flag(last)) return;
+    if (lane == 0) st_coh(ctr, 0u);
+#pragma unroll
+    for (int k = 0; k < kCS; ++k) T[k] = 0.0;
+    if (PART != kFinShared && in_range) sum_rows<kCS>(lvl1, tstride, (size_t)N, CS, n_cg, T);
+    tile_l = tile_a = 0.0;
+    if (blk) {
+      for (int g = lane; g < n_cg; g += 64) {
+        tile_l += ld_coh(blk1 + (size_t)g * l1_stride);
+        tile_a += ld_coh(blk1 + (size_t)g * l1_stride + 1);
+      }
+      tile_l = wave_sum_d(tile_l);
+      tile_a = wave_sum_d(tile_a);
+    }
+  }
 
   const bool valid = in_range;
   float lam = pr.lamb;
@@ -1619,15 +1711,16 @@ __device__ void fin_global(const pert_problem& pr, const pert_state& st, int n_b
 
 template <int K1T, int PART>
 __global__ void __launch_bounds__(kFinBlock) finalize_kernel(pert_problem pr, pert_state st, int n_cblk,
-                                                             int n_bt, int n_ct, int n_blk) {
+                                                             int n_bt, int n_ct, int n_blk, int n_cg) {
   // the device loop's stop flag is read first but tested only before the first store, so
   // its round trip overlaps the partial loads (a stopped launch writes nothing)
   const bool stopped = loop_stopped(st);
   __shared__ double s_g[kFinG][64];
   __shared__ int s_last;
   const int tid = threadIdx.x;
-  if ((int)blockIdx.x >= n_cblk) fin_bins(pr, st, blockIdx.x - n_cblk, n_ct, stopped, s_g);
-  else fin_cells<K1T, PART>(pr, st, blockIdx.x, n_bt, stopped, s_g);
+  const int n_cgb = n_cblk * n_cg;                         // cell-group blocks first, then bin blocks
+  if ((int)blockIdx.x >= n_cgb) fin_bins(pr, st, blockIdx.x - n_cgb, n_ct, stopped, s_g);
+  else fin_cells<K1T, PART>(pr, st, blockIdx.x / n_cg, n_bt, stopped, s_g, blockIdx.x % n_cg, n_cg);
   if (stopped || PART == kFinCells) return;                // (the cell half has no global sums)
   // Wave 0 wrote this block's outputs: publish them (agent-scope release), then count the
   // block in.  The last block to arrive acquires and runs the global sums, then re-arms
@@ -1700,48 +1793,6 @@ __device__ void loop_record(const pert_state& st) {
 // one workgroup hands to another goes through coherent (sc1) stores and loads, published by
 // a vmcnt wait before the counter RMW (st_coh / ld_coh below); every counter is re-armed by
 // the workgroup that consumed it.
-// bin tiles per level-0 group: about sqrt(n_bt), so both levels stay short (C4: 13 x 14,
-// C5 at LT 32: 66 x 65)
-__device__ __forceinline__ int fused_g1(int n_bt) {
-  int g = 8;
-  while (g * g < n_bt) ++g;
-  return g;
-}
-__device__ __forceinline__ int fused_n_g1(int n_bt) { const int g = fused_g1(n_bt); return (n_bt + g - 1) / g; }
-
-// s[k] += sum_{j < n} p[j rs + k ps] for k < np, in j order; 4-8 rows x NP planes of loads in
-// flight per round trip (clamped indices, masked values: no guarded loads); coherent loads
-template <int NP>
-__device__ __forceinline__ void sum_rows(const float* __restrict__ p, size_t rs, size_t ps, int np, int n,
-                                         double (&s)[NP]) {
-  constexpr int R = NP >= 6 ? 4 : 8;                        // rows per round trip
-  for (int j0 = 0; j0 < n; j0 += R) {
-    float v[R][NP];
-#pragma unroll
-    for (int u = 0; u < R; ++u)
-#pragma unroll
-      for (int k = 0; k < NP; ++k) {
-        const int j = j0 + u;
-        const float x = ld_coh(p + (size_t)min(j, n - 1) * rs + (size_t)min(k, np - 1) * ps);
-        v[u][k] = (j < n && k < np) ? x : 0.0f;
-      }
-#pragma unroll
-    for (int u = 0; u < R; ++u)
-#pragma unroll
-      for (int k = 0; k < NP; ++k) s[k] += (double)v[u][k];
-  }
-}
-
-// counters after finalize's arrival counter in cellblk_part: [n_ct][n_g1] group, [n_ct]
-// level-1, [n_bt] bin, [1] global
-__device__ __forceinline__ unsigned int* fused_counters(const pert_problem& pr, const pert_state& st) {
-  const int n_cblk = (pr.N + 63) / 64;
-  return reinterpret_cast<unsigned int*>(st.cellblk_part + (size_t)n_cblk * fin_slots(pr.n_libs, pr.K1) + 1);
-}
-
-__device__ __forceinline__ bool wave_flag(bool v) {
-  return __builtin_amdgcn_readfirstlane((int)v) != 0;
-}
 
 template <int K1T>
 __device__ void fused_cell_tile(const pert_problem& pr, const pert_state& st, const pert_adam_hparams& hp, int wt,
@@ -2462,12 +2513,23 @@ int launch_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream
   const int n_lblk = PART == kFinCells ? 0 : (prob->L + 63) / 64;
   const int n_cblk = (prob->N + 63) / 64;
   const int n_blk = prob->kind == PERT_KIND_STEP1 ? n_bt * n_ct : 0;   // observed pass only
+  // bin-tile groups of the per-cell reduction (fin_cells), as many as the workspace's level-1
+  // rows allow (pert_workspace_sizes: n_bt + n_g1 rows at the state's tile length)
+  int n_cg = 1;
+  if (PART != kFinShared) {
+    const int64_t n_bt_ws = (prob->L + tile_bins(st) - 1) / tile_bins(st);
+    int64_t g1 = 8;
+    while (g1 * g1 < n_bt_ws) ++g1;
+    const int64_t rows = n_bt_ws + (n_bt_ws + g1 - 1) / g1 - n_bt;
+    n_cg = (int)std::min<int64_t>((n_bt + kFinTPG - 1) / kFinTPG, std::max<int64_t>(rows, 1));
+  }
+  const dim3 grid(n_cblk * n_cg + n_lblk);
   if (prob->K1 == 5)
-    hipLaunchKernelGGL((finalize_kernel<5, PART>), dim3(n_cblk + n_lblk), dim3(kFinBlock), 0, stream, *prob, s2,
-                       n_cblk, n_bt, n_ct, n_blk);
+    hipLaunchKernelGGL((finalize_kernel<5, PART>), grid, dim3(kFinBlock), 0, stream, *prob, s2,
+                       n_cblk, n_bt, n_ct, n_blk, n_cg);
   else
-    hipLaunchKernelGGL((finalize_kernel<PERT_MAX_K1, PART>), dim3(n_cblk + n_lblk), dim3(kFinBlock), 0, stream,
-                       *prob, s2, n_cblk, n_bt, n_ct, n_blk);
+    hipLaunchKernelGGL((finalize_kernel<PERT_MAX_K1, PART>), grid, dim3(kFinBlock), 0, stream,
+                       *prob, s2, n_cblk, n_bt, n_ct, n_blk, n_cg);
   return hip_status(hipGetLastError());
 }
 

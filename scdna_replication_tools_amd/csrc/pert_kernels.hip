@@ -1325,6 +1325,45 @@ __device__ __forceinline__ void fin_bins(const pert_problem& pr, const pert_stat
   st.grad_shared[lay.off_rho + l] = (double)a_val * tot * (double)dmask;
 }
 
+// fin_bins with one wave per 64 bins (a workgroup takes 1024 bins): for a long genome over
+// few cell tiles (C5: 136 k bins x 32 tiles), where 64-bin workgroups of 16 waves loaded one
+// or two rows per wave in ~2,100 workgroups.  The same sums in the same order: the 16
+// interleaved groups of cell tiles (ct = g, g + 16, ...) each summed in tile order, then the
+// groups in order -- bit for bit fin_bins' result.
+__device__ __forceinline__ void fin_bins_wide(const pert_problem& pr, const pert_state& st, int lb, int n_ct,
+                                              bool stopped) {
+  const int tid = threadIdx.x;
+  const int L = pr.L;
+  const pert_layout lay = st.lay;
+  const int l = lb * kFinBlock + tid;
+  if (l >= L || stopped) return;
+  if (pr.kind == PERT_KIND_STEP3) { st.grad_shared[lay.off_rho + l] = 0.0; return; }
+  const float a_z = st.params[lay.off_a];
+  const float rho_z = st.params[lay.off_rho + l];
+  const float* __restrict__ bp = st.bin_part + l;
+  double tot = 0.0;
+  for (int g = 0; g < kFinG; ++g) {
+    // group g's tiles g, g + 16, ... in order, 4 loads in flight (fin_bins' kFinU rounds)
+    double sg = 0.0;
+    for (int c0 = g; c0 < n_ct; c0 += kFinG * 4) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int ct = c0 + u * kFinG;
+        const float x = bp[(size_t)min(ct, n_ct - 1) * L];
+        v[u] = ct < n_ct ? x : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sg += (double)v[u];
+    }
+    tot += sg;
+  }
+  const float a_val = fexp(a_z);
+  float dmask;
+  clipped_sigmoid(rho_z, &dmask);
+  st.grad_shared[lay.off_rho + l] = (double)a_val * tot * (double)dmask;
+}
+
 // ---- per-cell: the u / beta / tau priors (pert_model.py:585, :597-603) on top of the pass's
 // data sums T[k] (k < K1: sum_l gD omega g_k; k = K1: sum_l a gt) -> the ELBO's derivatives
 // for the cell's sites and its prior log density; dzbs / dbm: the cell's terms of the
@@ -1400,17 +1439,17 @@ __device__ __forceinline__ void cell_grads(int K1, bool step1, float c0, float u
 //              all-reduced (Adam then runs once both are done).
 constexpr int kFinAll = 0, kFinShared = 1, kFinCells = 2;
 
-// Groups (n_cg > 1): a cell block's bin tiles are split over n_cg workgroups of kFinTPG tiles
+// Groups (n_cg > 1): a cell block's bin tiles are split over n_cg workgroups of tpg tiles
 // (a genome of 20 kb bins has ~10^4 tiles: one workgroup per 64 cells walking them all left
 // the launch to 32 CUs at C5); each group's per-cell sums and ELBO / d/da sums go to a level-1
 // row (the rows after the bin tiles' in cell_part / blk_part, as pert_enum_step's), and the
 // group that arrives last adds the rows in group order and applies the priors.  n_cg == 1 is
-// the single-workgroup reduction, bit for bit.
-constexpr int kFinTPG = 128;
+// the single-workgroup reduction, bit for bit.  (fin_groups: only few cell blocks over many
+// tiles are split -- at C4, 157 blocks of 303 tiles, three groups made the launch 37 -> 52 us)
 
 template <int K1T, int PART = kFinAll>
 __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_state& st, int cb, int n_bt,
-                                          bool stopped, double (*s_g)[64], int grp_c = 0, int n_cg = 1) {
+                                          bool stopped, double (*s_g)[64], int grp_c = 0, int n_cg = 1, int tpg = 0) {
   constexpr int kCS = K1T + 1;
   constexpr int kFinU = K1T <= 5 ? PERT_FIN_U : 1;   // bin tiles in flight per thread
   const int tid = threadIdx.x, lane = tid & 63, grp = tid >> 6;
@@ -1443,8 +1482,8 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
       }
   }
   // this group's bin tiles [t0, t1) (all of them when n_cg == 1)
-  const int t0 = n_cg > 1 ? grp_c * kFinTPG : 0;
-  const int t1 = n_cg > 1 ? min(n_bt, t0 + kFinTPG) : n_bt;
+  const int t0 = n_cg > 1 ? grp_c * tpg : 0;
+  const int t1 = n_cg > 1 ? min(n_bt, t0 + tpg) : n_bt;
   // the enumerated pass's ELBO / d/da sums of this cell tile, one bin tile per thread
   double wl = 0.0, wa = 0.0;
   const size_t bstride = (size_t)(pr.ldn / 64) * kBlkSlots;
@@ -1711,7 +1750,8 @@ __device__ void fin_global(const pert_problem& pr, const pert_state& st, int n_b
 
 template <int K1T, int PART>
 __global__ void __launch_bounds__(kFinBlock) finalize_kernel(pert_problem pr, pert_state st, int n_cblk,
-                                                             int n_bt, int n_ct, int n_blk, int n_cg) {
+                                                             int n_bt, int n_ct, int n_blk, int n_cg, int tpg,
+                                                             int bins_wide) {
   // the device loop's stop flag is read first but tested only before the first store, so
   // its round trip overlaps the partial loads (a stopped launch writes nothing)
   const bool stopped = loop_stopped(st);
@@ -1719,8 +1759,12 @@ __global__ void __launch_bounds__(kFinBlock) finalize_kernel(pert_problem pr, pe
   __shared__ int s_last;
   const int tid = threadIdx.x;
   const int n_cgb = n_cblk * n_cg;                         // cell-group blocks first, then bin blocks
-  if ((int)blockIdx.x >= n_cgb) fin_bins(pr, st, blockIdx.x - n_cgb, n_ct, stopped, s_g);
-  else fin_cells<K1T, PART>(pr, st, blockIdx.x / n_cg, n_bt, stopped, s_g, blockIdx.x % n_cg, n_cg);
+  if ((int)blockIdx.x >= n_cgb) {
+    if (bins_wide) fin_bins_wide(pr, st, blockIdx.x - n_cgb, n_ct, stopped);
+    else fin_bins(pr, st, blockIdx.x - n_cgb, n_ct, stopped, s_g);
+  } else {
+    fin_cells<K1T, PART>(pr, st, blockIdx.x / n_cg, n_bt, stopped, s_g, blockIdx.x % n_cg, n_cg, tpg);
+  }
   if (stopped || PART == kFinCells) return;                // (the cell half has no global sums)
   // Wave 0 wrote this block's outputs: publish them (agent-scope release), then count the
   // block in.  The last block to arrive acquires and runs the global sums, then re-arms
@@ -2515,21 +2559,29 @@ int launch_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream
   const int n_blk = prob->kind == PERT_KIND_STEP1 ? n_bt * n_ct : 0;   // observed pass only
   // bin-tile groups of the per-cell reduction (fin_cells), as many as the workspace's level-1
   // rows allow (pert_workspace_sizes: n_bt + n_g1 rows at the state's tile length)
-  int n_cg = 1;
-  if (PART != kFinShared) {
+  // only few cell blocks over many tiles are split: about one workgroup per CU in all, groups
+  // of at least 256 tiles (C5 2,000 cells: 8 groups; its 250-cell shard: 30; C4: none)
+  int n_cg = 1, tpg = n_bt;
+  if (PART != kFinShared && n_cblk < 128 && n_bt >= 1024) {
     const int64_t n_bt_ws = (prob->L + tile_bins(st) - 1) / tile_bins(st);
     int64_t g1 = 8;
     while (g1 * g1 < n_bt_ws) ++g1;
     const int64_t rows = n_bt_ws + (n_bt_ws + g1 - 1) / g1 - n_bt;
-    n_cg = (int)std::min<int64_t>((n_bt + kFinTPG - 1) / kFinTPG, std::max<int64_t>(rows, 1));
+    const int64_t want = std::min<int64_t>((256 + n_cblk - 1) / n_cblk, (n_bt + 255) / 256);
+    const int64_t cg = std::max<int64_t>(1, std::min<int64_t>(want, rows));
+    tpg = (int)((n_bt + cg - 1) / cg);
+    n_cg = (int)((n_bt + tpg - 1) / tpg);
   }
-  const dim3 grid(n_cblk * n_cg + n_lblk);
+  // the bin blocks: 1,024 bins each when the genome is long against the cell tiles
+  const int bins_wide = (PART != kFinCells && n_lblk > 512 && n_ct <= 64) ? 1 : 0;
+  const int n_bblk = bins_wide ? (prob->L + kFinBlock - 1) / kFinBlock : n_lblk;
+  const dim3 grid(n_cblk * n_cg + n_bblk);
   if (prob->K1 == 5)
     hipLaunchKernelGGL((finalize_kernel<5, PART>), grid, dim3(kFinBlock), 0, stream, *prob, s2,
-                       n_cblk, n_bt, n_ct, n_blk, n_cg);
+                       n_cblk, n_bt, n_ct, n_blk, n_cg, tpg, bins_wide);
   else
     hipLaunchKernelGGL((finalize_kernel<PERT_MAX_K1, PART>), grid, dim3(kFinBlock), 0, stream,
-                       *prob, s2, n_cblk, n_bt, n_ct, n_blk, n_cg);
+                       *prob, s2, n_cblk, n_bt, n_ct, n_blk, n_cg, tpg, bins_wide);
   return hip_status(hipGetLastError());
 }
 

@@ -21,6 +21,7 @@
 
 #include <math.h>
 #include <stddef.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <mutex>
@@ -2562,7 +2563,19 @@ int launch_finalize(const pert_problem* prob, pert_state* st, hipStream_t stream
   // only few cell blocks over many tiles are split: about one workgroup per CU in all, groups
   // of at least 256 tiles (C5 2,000 cells: 8 groups; its 250-cell shard: 30; C4: none)
   int n_cg = 1, tpg = n_bt;
-  if (PART != kFinShared && n_cblk < 128 && n_bt >= 1024) {
+  static const int forced = [] {                 // PERT_FIN_GROUPS=<n>: a fixed group count (A/B runs)
+    const char* e = getenv("PERT_FIN_GROUPS");
+    return e ? atoi(e) : 0;
+  }();
+  if (PART != kFinShared && forced > 1 && n_bt >= 2 * forced) {
+    const int64_t n_bt_ws = (prob->L + tile_bins(st) - 1) / tile_bins(st);
+    int64_t g1 = 8;
+    while (g1 * g1 < n_bt_ws) ++g1;
+    const int64_t rows = n_bt_ws + (n_bt_ws + g1 - 1) / g1 - n_bt;
+    const int64_t cg = std::max<int64_t>(1, std::min<int64_t>(forced, rows));
+    tpg = (int)((n_bt + cg - 1) / cg);
+    n_cg = (int)((n_bt + tpg - 1) / tpg);
+  } else if (PART != kFinShared && forced == 0 && n_cblk < 128 && n_bt >= 1024) {
     const int64_t n_bt_ws = (prob->L + tile_bins(st) - 1) / tile_bins(st);
     int64_t g1 = 8;
     while (g1 * g1 < n_bt_ws) ++g1;

@@ -80,3 +80,48 @@ def test_native_sharded_loop_matches_python_sharded_loop(comm, kind, fused, even
     if events:
         assert len(a.pass_events) >= len(la) // 3
     comm.set_options()
+
+
+def test_rccl_comm_fault_aborts_and_a_new_comm_works():
+    """The RCCL backend's failure path at world 1 (the only RCCL world a one-GPU box has): an
+    all-reduce that cannot be queued (pert_comm_inject_fault) makes the C loop abort the
+    communicator (ncclCommAbort) and raise CommError instead of hanging; the aborted comm
+    refuses further work, closes cleanly, and a new communicator fits normally."""
+    from scdna_replication_tools_amd import _native as nat
+    from scdna_replication_tools_amd.engine import RcclComm
+    prob, kw, z = make_problem("step2", seed=4)
+    c = RcclComm.world1()
+    a = _shard("step2", kw, z, comm=c)
+    c.inject_fault(13)                               # iteration 12 (call 0: the shard's set-up all-reduce)
+    with pytest.raises(nat.CommError) as e:
+        a.run_svi(40, 10 ** 9, 0.0)
+    assert e.value.code == nat.E_COMM_FAULT
+    assert c.status() == nat.E_COMM_FAULT
+    assert a.last_launched == 8                      # the first chunk was queued whole, the second not
+    with pytest.raises(nat.CommError):
+        a.run_svi(8, 10 ** 9, 0.0)                   # the aborted comm refuses further work
+    c.close()
+    c2 = RcclComm.world1()
+    b = _shard("step2", kw, z, comm=c2)
+    ref = _shard("step2", kw, z, allreduce=lambda t: None)
+    lb, _ = b.run_svi(20, 10 ** 9, 0.0)
+    lr, _ = ref.run_svi(20, 10 ** 9, 0.0)
+    assert np.array_equal(np.asarray(lb), np.asarray(lr))
+    c2.close()
+
+
+def test_rccl_comm_raised_abort_word_stops_the_loop():
+    """A raised abort word (what a failed peer on the node does) makes the loop return
+    PERT_E_COMM_ABORTED at its first wait."""
+    from scdna_replication_tools_amd import _native as nat
+    from scdna_replication_tools_amd.engine import RcclComm
+    prob, kw, z = make_problem("step2", seed=4)
+    c = RcclComm.world1()
+    a = _shard("step2", kw, z, comm=c)
+    c.abort(nat.E_COMM_ABORTED)
+    t0 = time.perf_counter()
+    with pytest.raises(nat.CommError) as e:
+        a.run_svi(40, 10 ** 9, 0.0)
+    assert e.value.code == nat.E_COMM_ABORTED
+    assert time.perf_counter() - t0 < 10.0
+    c.close()

@@ -1151,14 +1151,14 @@ class PertShard:
                 nl = ctypes.c_int32(0)
                 fn = self._lib_chunk.pert_svi_run_sharded if native_comm else self._lib_chunk.pert_svi_run
                 with self._dev():
-                    nat.check(fn(
-                        ctypes.byref(self._prob), ctypes.byref(st), ctypes.byref(self._hp),
-                        ss.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
-                        ib.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n, chunk, depth,
-                        1 if self.fused else 0, *shard_args, evp, host.data_ptr(), ctypes.byref(nl),
-                        self._stream()), "pert_svi_run")
+                    rc = fn(ctypes.byref(self._prob), ctypes.byref(st), ctypes.byref(self._hp),
+                            ss.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                            ib.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n, chunk, depth,
+                            1 if self.fused else 0, *shard_args, evp, host.data_ptr(), ctypes.byref(nl),
+                            self._stream())
                 launched = int(nl.value)
-                self.last_launched = launched
+                self.last_launched = launched          # (also when the loop failed)
+                nat.check(rc, "pert_svi_run")
                 # the stop from the copied records (every launched iteration's record is in
                 # pinned memory once the call returns; the first marked one is the stop --
                 # loop_ctl[0] -- and a NaN loss there is reason 2), no device read-back

@@ -316,14 +316,7 @@ int pert_comm_init_host(const char* name, int32_t world, int32_t rank, int64_t m
     return rc;
   }
   c->own_abort_word = true;
-  if (hipHostMalloc(&c->pin_send, sizeof(double) * max_n, hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc(&c->pin_recv, sizeof(double) * max_n, hipHostMallocDefault) != hipSuccess) {
-    if (c->pin_send) (void)hipHostFree(c->pin_send);
-    munmap(c->seg.base, c->seg.bytes);
-    delete c;
-    return PERT_E_HIP_BASE + (int)hipErrorOutOfMemory;
-  }
-  *out = c;
+  *out = c;                                   // (the pinned buffers come with the first all-reduce)
   return PERT_OK;
 }
 
@@ -456,6 +449,15 @@ int pert_comm_allreduce_sum_f64(pert_comm* c, const double* send, double* recv, 
   }
   if (c->kind == kKindHost) {
     if (n > c->seg.max_n) return PERT_E_ARG;
+    if (!c->pin_send) {
+      hipError_t e = hipHostMalloc(&c->pin_send, sizeof(double) * c->seg.max_n, hipHostMallocDefault);
+      if (e == hipSuccess) e = hipHostMalloc(&c->pin_recv, sizeof(double) * c->seg.max_n, hipHostMallocDefault);
+      if (e != hipSuccess) {
+        if (c->pin_send) (void)hipHostFree(c->pin_send);
+        c->pin_send = c->pin_recv = nullptr;
+        return hip_rc(e);
+      }
+    }
     hipError_t e = hipMemcpyAsync(c->pin_send, send, sizeof(double) * n, hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipLaunchHostFunc(stream, host_sum, new HostCall{c, n});
     if (e == hipSuccess) e = hipMemcpyAsync(recv, c->pin_recv, sizeof(double) * n, hipMemcpyHostToDevice, stream);

@@ -305,3 +305,49 @@ def test_online_low_coverage_matches_cellbin(nat, dlo, dhi):
     assert (np.abs(onl["E"] - fwd["E"]) / scale).max() < 1e-5
     g_scale = np.maximum(1.0, np.abs(fwd["gz"]).max(1, keepdims=True))
     assert (np.abs(onl["gz"] - fwd["gz"]) / g_scale).max() < 1e-5
+
+
+def _host_comm_rank(rank, name, q):
+    import ctypes
+    import time
+    from scdna_replication_tools_amd import _native
+    lib = _native.lib_nogil()
+    h = ctypes.c_void_p()
+    rc = lib.pert_comm_init_host(name, 2, rank, 16, 10.0, ctypes.byref(h))
+    out = {"init": rc}
+    if rc == 0:
+        if rank == 1:
+            time.sleep(0.2)
+            out["abort"] = lib.pert_comm_abort(h, _native.E_COMM_FAULT)
+            out["status"] = lib.pert_comm_status(h)
+        else:
+            t0 = time.time()
+            st = 0
+            while st == 0 and time.time() - t0 < 10.0:
+                st = lib.pert_comm_status(h)
+                time.sleep(0.01)
+            out["status"], out["waited"] = st, time.time() - t0
+        out["destroy"] = lib.pert_comm_destroy(h)
+    q.put((rank, out))
+
+
+def test_host_comm_two_processes_share_the_abort_word(nat):
+    """Two processes attach one host-staged communicator (no GPU needed before the first
+    all-reduce): the segment is unlinked once both have mapped it, and an abort raised by rank 1
+    is seen by rank 0 as PERT_E_COMM_ABORTED -- the word a failed rank's peers poll."""
+    import multiprocessing as mp
+    import os
+    name = "/pert-test2-{}".format(os.getpid()).encode()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_host_comm_rank, args=(r, name, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=60) for _ in range(2))
+    for p in ps:
+        p.join(timeout=30)
+    assert got[0]["init"] == 0 and got[1]["init"] == 0, got
+    assert not os.path.exists("/dev/shm" + name.decode())
+    assert got[1]["abort"] == 0 and got[1]["status"] == nat.E_COMM_FAULT
+    assert got[0]["status"] == nat.E_COMM_ABORTED and got[0]["waited"] < 10.0
+    assert got[0]["destroy"] == 0 and got[1]["destroy"] == 0

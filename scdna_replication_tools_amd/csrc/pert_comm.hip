@@ -113,7 +113,7 @@ int attach_segment(const char* name, int32_t world, int32_t rank, int64_t max_n,
   for (int64_t k = 0; s.attached().load(std::memory_order_acquire) < world; ++k) {
     if (now_s() - t0 > timeout_s) {
       munmap(p, bytes);
-      if (rank == 0) shm_unlink(name);
+      shm_unlink(name);                       // (every rank: a late one may have re-created it)
       return PERT_E_COMM_TIMEOUT;
     }
     backoff(k);

@@ -328,11 +328,12 @@ def main():
                          "g1_composite (the reference's default; the product's composite code book, many rows)")
     ap.add_argument("--event-stride", type=int, default=5,
                     help="HIP events around the pass of every k-th step of the pass-timing run (1: every step)")
-    ap.add_argument("--comm", default="auto", choices=["auto", "rccl", "torch"],
+    ap.add_argument("--comm", default="auto", choices=["auto", "rccl", "torch", "host"],
                     help="cross-rank sum of the shared block: 'rccl' = the library's own RCCL communicator "
                          "(pert_comm, queued inside the C loop; the default on N > 1 over nccl, and at N = 1 "
                          "it times the sharded step with a one-rank all-reduce), 'torch' = torch.distributed "
-                         "per step from Python")
+                         "per step from Python, 'host' = the library's host-staged communicator (ranks sharing "
+                         "a GPU: a rehearsal of the N > 1 C loop with PERT_DIST_BACKEND=gloo)")
     ap.add_argument("--comm-overlap", type=int, default=0,
                     help="1: the sharded step split so the all-reduce overlaps the per-cell finalize on a side "
                          "stream (pert_comm_allreduce_async); 0 (default; faster on ROCm 7.2): finalize, "
@@ -374,7 +375,7 @@ def main():
             dist.init_process_group(backend)
         pg = dist
 
-    from scdna_replication_tools_amd.engine import EtaCodebook, PertShard, RcclComm
+    from scdna_replication_tools_amd.engine import EtaCodebook, HostComm, PertShard, RcclComm
     from scdna_replication_tools_amd.init import init_params
     from scdna_replication_tools_amd.sharding import cell_bounds, make_allreduce
 
@@ -410,7 +411,11 @@ def main():
         prior_desc = "g1_clones (weight 1e6)"
     ploidy = eta.argmax_states().mean(0)
     comm, comm_error = None, None
-    if args.comm == "rccl" or (args.comm == "auto" and world > 1 and backend == "nccl"):
+    if args.comm == "host":
+        if world < 2:
+            raise SystemExit("--comm host needs torch.distributed ranks (world > 1)")
+        comm = HostComm()
+    elif args.comm == "rccl" or (args.comm == "auto" and world > 1 and backend == "nccl"):
         try:
             comm = RcclComm() if world > 1 else RcclComm.world1()
         except Exception as e:                     # noqa: BLE001  (then torch.distributed's all-reduce)
@@ -422,7 +427,8 @@ def main():
     if comm is not None:
         comm.set_options(overlap=bool(args.comm_overlap), delay_us=args.comm_delay_us)
     allreduce = comm.allreduce if comm is not None else make_allreduce()
-    comm_desc = ("rccl: the library's own communicator, all-reduce queued inside the C loop (pert_svi_run_sharded)"
+    comm_desc = (("host-staged: the library's shared-memory communicator" if args.comm == "host" else
+                  "rccl: the library's own communicator") + ", all-reduce queued inside the C loop (pert_svi_run_sharded)"
                  if comm is not None else "torch.distributed all_reduce per step from Python{}".format(
                      " (pert_comm failed: {})".format(comm_error) if comm_error else "") if allreduce is not None
                  else "none (one rank)")

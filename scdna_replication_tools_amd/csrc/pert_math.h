@@ -103,6 +103,9 @@ PERT_HD float log1p_corr(float q, float inv_u) {
 #ifndef PERT_SHIFT_N
 #define PERT_SHIFT_N 2             // (A/B builds: -DPERT_SHIFT_N=4 is round 5's threshold 5 / shift 4)
 #endif
+#ifndef PERT_PACKED_SHIFT
+#define PERT_PACKED_SHIFT 1
+#endif
 constexpr int kShiftN = PERT_SHIFT_N;   // 1 <= d < kAsymMin is shifted by kShiftN (d + kShiftN >= kAsymMin)
 constexpr float kAsymMin = 1.0f + kShiftN;   // asymptotic series used for arguments >= kAsymMin
 constexpr float kShift = (float)kShiftN;
@@ -199,6 +202,51 @@ PERT_HD void nb_asym_pair_direct(pf2 chi, float D, float x, float invx, float lo
   const pf2 r4 = r2 * r2, rz4 = rz2 * rz2;
   const pf2 psi = l1 - 0.5f * (rz - r) - 0.0833333333333333333f * (rz2 - r2)
                   + 0.00833333333333333333f * (rz4 - r4) - 0.00396825396825396825f * (rz4 * rz2 - r4 * r2);
+  nchi = d * log1m_lam + lam;
+  bc = chi * (psi + log1m_lam);
+}
+
+// nb_asym_pair_direct for a chain pair whose deltas are >= 1 on every lane but below kAsymMin on
+// some (low coverage): per element, d < kAsymMin is shifted by kShiftN = 2 in closed form --
+// A = d (d + 1), A' = 2 d + 1, B = (d + x)(d + x + 1), B' = 2 (d + x) + 1 (nb_shift's products for
+// two factors) -- the series evaluated at the shifted argument, the corrections -log(B / A) and
+// A'/A - B'/B added where shifted (zero where x == 0, as nb_shift), all in packed fp32
+// (PERT_PACKED_SHIFT; 2 v_rcp + 1 v_log per shifted element as nb_shift, no divergent branch).
+PERT_HD void nb_shift_pair_direct(pf2 chi, float D, float x, float invx, float log1m_lam, pf2& nchi, pf2& bc) {
+  const pf2 d = chi * D;
+  const bool s0 = d.x < kAsymMin, s1 = d.y < kAsymMin;
+  const pf2 ds = {s0 ? d.x + kShift : d.x, s1 ? d.y + kShift : d.y};
+  // the series at ds (nb_asym_pair_direct's arithmetic)
+  const pf2 r = {frcp(ds.x), frcp(ds.y)};
+  const pf2 zs = ds + x;
+  const pf2 rz = {frcp(zs.x), frcp(zs.y)};
+  const pf2 q = r * x;
+  const pf2 iu = ds * rz;
+  const pf2 u = q + 1.0f;
+  const pf2 lu = pf2{__builtin_amdgcn_logf_or_log2(u.x), __builtin_amdgcn_logf_or_log2(u.y)} * kLn2;
+  const pf2 l1 = lu + (q - (u - 1.0f)) * iu;
+  const pf2 q2 = ds * invx;
+  const pf2 u2 = q2 + 1.0f;
+  const pf2 lu2 = pf2{__builtin_amdgcn_logf_or_log2(u2.x), __builtin_amdgcn_logf_or_log2(u2.y)} * kLn2;
+  const pf2 l2 = lu2 + (q2 - (u2 - 1.0f)) * (rz * x);
+  const pf2 r2 = r * r, rz2 = rz * rz;
+  const pf2 sr = r * (0.0833333333333333333f - r2 * (0.00277777777777777778f - r2 * 0.000793650793650793651f));
+  const pf2 srz = rz * (0.0833333333333333333f - rz2 * (0.00277777777777777778f - rz2 * 0.000793650793650793651f));
+  pf2 lam = (ds - 0.5f) * l1 + x * l2 + (srz - sr);
+  const pf2 r4 = r2 * r2, rz4 = rz2 * rz2;
+  pf2 psi = l1 - 0.5f * (rz - r) - 0.0833333333333333333f * (rz2 - r2)
+            + 0.00833333333333333333f * (rz4 - r4) - 0.00396825396825396825f * (rz4 * rz2 - r4 * r2);
+  // the shift's corrections at d (2 factors)
+  const pf2 A = d * (d + 1.0f), Ap = 2.0f * d + 1.0f;
+  const pf2 b = d + x;
+  const pf2 B = b * (b + 1.0f), Bp = 2.0f * b + 1.0f;
+  const pf2 rA = {frcp(A.x), frcp(A.y)}, rB = {frcp(B.x), frcp(B.y)};
+  const pf2 BA = B * rA;
+  const pf2 cl = pf2{__builtin_amdgcn_logf_or_log2(BA.x), __builtin_amdgcn_logf_or_log2(BA.y)} * -kLn2;
+  const pf2 cp = Ap * rA - Bp * rB;
+  const bool xp = x > 0.0f;
+  lam += pf2{(s0 && xp) ? cl.x : 0.0f, (s1 && xp) ? cl.y : 0.0f};
+  psi += pf2{(s0 && xp) ? cp.x : 0.0f, (s1 && xp) ? cp.y : 0.0f};
   nchi = d * log1m_lam + lam;
   bc = chi * (psi + log1m_lam);
 }
@@ -656,6 +704,17 @@ PERT_HD void enum_online(float x, float invx, const float (&z)[P], float log1m_l
               bb[j1] = b2.y;
               pdone[decltype(pc)::value] = true;
             }
+#if PERT_PACKED_SHIFT
+            else if (wave_all((float)c0 * D >= 1.0f)) {   // no clamp on any lane: shifted where needed
+              pf2 n2, b2;
+              nb_shift_pair_direct(pf2{(float)c0, (float)c1}, D, x, invx, log1m_lam, n2, b2);
+              nn[j0] = n2.x;
+              bb[j0] = b2.x;
+              nn[j1] = n2.y;
+              bb[j1] = b2.y;
+              pdone[decltype(pc)::value] = true;
+            }
+#endif
           }
         });
       }

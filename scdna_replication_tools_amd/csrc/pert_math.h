@@ -104,7 +104,7 @@ PERT_HD float log1p_corr(float q, float inv_u) {
 #define PERT_SHIFT_N 2             // (A/B builds: -DPERT_SHIFT_N=4 is round 5's threshold 5 / shift 4)
 #endif
 #ifndef PERT_PACKED_SHIFT
-#define PERT_PACKED_SHIFT 1
+#define PERT_PACKED_SHIFT 0
 #endif
 constexpr int kShiftN = PERT_SHIFT_N;   // 1 <= d < kAsymMin is shifted by kShiftN (d + kShiftN >= kAsymMin)
 constexpr float kAsymMin = 1.0f + kShiftN;   // asymptotic series used for arguments >= kAsymMin
@@ -212,6 +212,10 @@ PERT_HD void nb_asym_pair_direct(pf2 chi, float D, float x, float invx, float lo
 // two factors) -- the series evaluated at the shifted argument, the corrections -log(B / A) and
 // A'/A - B'/B added where shifted (zero where x == 0, as nb_shift), all in packed fp32
 // (PERT_PACKED_SHIFT; 2 v_rcp + 1 v_log per shifted element as nb_shift, no divergent branch).
+// Measured in round 6 and off: it compiles to the same 168 VGPRs, and is correct (GPU parity,
+// edge, configs and chain suites green with it), but C5's step is 0.7 % and its 250-cell
+// shard's 2 % slower (profiles/r06ab) -- every lane of the pair pays the shift's products and
+// logarithm, where the per-chain path skips them on the lanes already past the threshold.
 PERT_HD void nb_shift_pair_direct(pf2 chi, float D, float x, float invx, float log1m_lam, pf2& nchi, pf2& bc) {
   const pf2 d = chi * D;
   const bool s0 = d.x < kAsymMin, s1 = d.y < kAsymMin;

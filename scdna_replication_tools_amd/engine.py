@@ -493,8 +493,9 @@ class HostComm(PertComm):
         self.lib = nat.lib_nogil()
         self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
         name = _broadcast_bytes(_segment_name().encode() if self.rank == 0 else b"", 64, group).rstrip(b"\0")
+        self.max_n = int(max_n)
         h = ctypes.c_void_p()
-        nat.check(self.lib.pert_comm_init_host(name, self.world, self.rank, int(max_n), comm_timeout_s(),
+        nat.check(self.lib.pert_comm_init_host(name, self.world, self.rank, self.max_n, comm_timeout_s(),
                                                ctypes.byref(h)), "pert_comm_init_host")
         self.handle = h
         self._fault_from_env()
@@ -652,6 +653,9 @@ class PertShard:
         # ---- packed parameters (include/pert_hip.h pert_layout)
         self.lay = nat.make_layout(L, N, self.K1, self.n_libs)
         lay = self.lay
+        if comm is not None and getattr(comm, "max_n", None) is not None and lay.n_shared + 1 > comm.max_n:
+            raise ValueError("the shared block ({} doubles) exceeds the host communicator's max_n ({}): "
+                             "make HostComm(max_n=...) larger".format(lay.n_shared + 1, comm.max_n))
         self.params = torch.zeros(lay.n_params, **f32)
         self.adam_m = torch.zeros(lay.n_params, **f32)
         self.adam_v = torch.zeros(lay.n_params, **f32)

@@ -36,6 +36,19 @@ def main():
                     help="oracle per-step timing sample (0: skip the CPU extrapolation)")
     args = ap.parse_args()
     import torch
+    # under torch.distributed.run (WORLD_SIZE > 1): the fit cell-sharded over the ranks
+    # (pert_model._Dist); PERT_DIST_BACKEND=gloo with PERT_NATIVE_COMM=host rehearses an
+    # N-GPU node's C loop with the ranks sharing GPU 0.  Rank 0 prints the record.
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    fit_kw = {}
+    if world > 1:
+        import torch.distributed as dist
+        backend = os.environ.get("PERT_DIST_BACKEND", "nccl")
+        dev = 0 if backend == "gloo" else int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(dev)
+        dist.init_process_group(backend)
+        fit_kw["device"] = "cuda:{}".format(dev)
     from scdna_replication_tools_amd.pert_model import pert_infer_scRT
     from scdna_replication_tools_amd.simulator import simulate, to_long_form
     n, nb, sub = CONFIGS[args.config]
@@ -73,7 +86,7 @@ def main():
     else:
         m = pert_infer_scRT(df_s, df_g, input_col='reads', clone_col='clone_id', cn_prior_method=args.prior,
                             max_iter=args.max_iter, min_iter=args.min_iter, run_step3=not args.no_step3,
-                            n_jobs=args.n_jobs)
+                            n_jobs=args.n_jobs, **fit_kw)
         cn_s_out, supp_s, cn_g1_out, supp_g1 = m.run_pert_model()
         clusters_ok = None
     beat.set()
@@ -90,6 +103,13 @@ def main():
     if clusters_ok is not None:
         rec["clusters_match_truth"] = clusters_ok
         rec["n_clusters"] = int(sc.clusters["cluster_id"].nunique())
+    if world > 1:
+        rec["ranks"] = {"world": world, "backend": os.environ.get("PERT_DIST_BACKEND", "nccl"),
+                        "native_comm": os.environ.get("PERT_NATIVE_COMM", "1"), "launched": m.launched}
+        import torch.distributed as dist
+        dist.destroy_process_group()
+        if rank != 0:
+            return
     if args.cpu_sample_cells > 0:
         print("timing the CPU oracle on {} cells".format(args.cpu_sample_cells), file=sys.stderr, flush=True)
         from bench import cpu_extrapolation           # bench.py's cpu_baseline leg (the oracle)

@@ -1235,6 +1235,9 @@ constexpr int kFinG = kFinBlock / 64;
 #ifndef PERT_FIN_U
 #define PERT_FIN_U 4
 #endif
+#ifndef PERT_FIN_COH
+#define PERT_FIN_COH 1
+#endif
 __host__ __device__ constexpr int fin_slots(int n_libs, int K1) { return 2 * n_libs * K1 + 2; }
 
 // bin tiles per level-0 group: about sqrt(n_bt), so both levels stay short (C4: 13 x 14,
@@ -1627,7 +1630,12 @@ __device__ __forceinline__ void fin_cells(const pert_problem& pr, const pert_sta
       val = sl == 2 * nl * K1 ? lp : 0.0;
     }
     val = wave_sum_d(val);
-    if (lane == 0) out[sl] = val + (sl == 2 * nl * K1 ? tile_l : (sl == 2 * nl * K1 + 1 ? tile_a : 0.0));
+    const double v = val + (sl == 2 * nl * K1 ? tile_l : (sl == 2 * nl * K1 + 1 ? tile_a : 0.0));
+#if PERT_FIN_COH
+    if (lane == 0) st_coh(out + sl, v);                    // read by this launch's last block
+#else
+    if (lane == 0) out[sl] = v;
+#endif
   }
 }
 
@@ -1672,7 +1680,14 @@ __device__ void fin_global(const pert_problem& pr, const pert_state& st, int n_b
     for (int b0 = lane; b0 < n_cblk; b0 += 64 * kGU) {
       double q[kGU];
 #pragma unroll
-      for (int u = 0; u < kGU; ++u) q[u] = st.cellblk_part[(size_t)min(b0 + 64 * u, n_cblk - 1) * nslot + sl];
+      for (int u = 0; u < kGU; ++u) {
+        const double* slot = st.cellblk_part + (size_t)min(b0 + 64 * u, n_cblk - 1) * nslot + sl;
+#if PERT_FIN_COH
+        q[u] = ld_coh(slot);
+#else
+        q[u] = *slot;
+#endif
+      }
 #pragma unroll
       for (int u = 0; u < kGU; ++u)
         if (b0 + 64 * u < n_cblk) acc += q[u];
@@ -1767,17 +1782,26 @@ __global__ void __launch_bounds__(kFinBlock) finalize_kernel(pert_problem pr, pe
     fin_cells<K1T, PART>(pr, st, blockIdx.x / n_cg, n_bt, stopped, s_g, blockIdx.x % n_cg, n_cg, tpg);
   }
   if (stopped || PART == kFinCells) return;                // (the cell half has no global sums)
-  // Wave 0 wrote this block's outputs: publish them (agent-scope release), then count the
-  // block in.  The last block to arrive acquires and runs the global sums, then re-arms
-  // the counter for the next launch.
+  // Wave 0 wrote this block's outputs: publish them, then count the block in.  The last block
+  // to arrive runs the global sums, then re-arms the counter for the next launch.  (PERT_FIN_COH:
+  // the only outputs the last block reads, the cell blocks' slots, are coherent sc1 stores, so
+  // publishing is a vmcnt wait -- as pert_enum_step's hand-offs -- not an agent-scope fence,
+  // which writes back the XCD's L2 once per workgroup: round 6 measured the shared half of a
+  // 1,250-cell finalize at 14-15 of its 19-22 us.)
+#if PERT_FIN_COH
+  if (tid < 64) publish_wait();
+#else
   if (tid < 64) __threadfence();
+#endif
   __syncthreads();
   unsigned int* arrivals = reinterpret_cast<unsigned int*>(
       st.cellblk_part + (size_t)n_cblk * fin_slots(pr.n_libs, pr.K1));
   if (tid == 0) s_last = atomicAdd(arrivals, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!s_last) return;
+#if !PERT_FIN_COH
   __threadfence();
+#endif
   fin_global(pr, st, n_blk, n_cblk);
   if (tid == 0) atomicExch(arrivals, 0u);
 }
